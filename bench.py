@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Benchmark of the SRC -> 6-biquad EQ -> FFT chain on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+Workload (BASELINE.json configs[2]): per GPU, 4096
+channels x 48000 samples at 48 kHz, SRC L=3/M=2 with the default 121-tap
+sinc x Blackman FIR, the 6-band EQ with gains {+6, -4, +3, -3, +5, -6} dB at
+fs' = 72 kHz, and a 4096-point Hann-windowed FFT magnitude of the centre
+segment of z.  Input is synthetic uniform(-1, 1) float32 generated on the
+device (the reference's example WAVs are missing), resident in HBM before the
+timed region.  One step = one pass of the chain over the batch.  Channels shard
+over ranks with no collective (weak scaling: 4096 channels per GPU, so N = 8
+is config 4's 32768 channels); the only cross-rank calls are the timing
+barrier and the max-over-ranks of the elapsed time.
+
+Rank 0 prints one JSON line.  Besides the contract fields it carries
+`roofline` (dominant kernel, algorithmic bytes per launch / its mean duration
+from HIP events recorded around every launch in a traced pass), `chain_roofline`
+(whole-chain algorithmic bytes / ms_per_step) and, at N = 1, `cpu_baseline`:
+the repo's CPU oracle (same numpy/scipy calls as the reference's dsp_core.py)
+timed on a bounded channel sample with a process pool, measured BEFORE the GPU
+is initialised.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "dsp-audio-project_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "Msamples/sec SRC→6-biquad EQ→FFT chain at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CONFIG3_GAINS = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3,
+                 "High Mids": -3, "Presence": 5, "Brilliance": -6}
+
+WORKLOADS = {
+    "c3": dict(name="config3", n_in=48000, fs=48000, L=3, M=2, num_taps=None, n_fft=4096,
+               channels=4096,
+               desc="4096 ch x 48000 @48kHz: SRC L3/M2 K121 -> 6-biquad EQ @72kHz -> "
+                    "4096-pt FFT |X| of centre segment"),
+    "c5": dict(name="config5", n_in=48000, fs=44100, L=160, M=147, num_taps=1023, n_fft=4096,
+               channels=1024,
+               desc="1024 ch/GPU x 48000 @44.1kHz: SRC L160/M147 K1023 -> 6-biquad EQ @48kHz -> "
+                    "4096-pt FFT |X| (config 5 = 8192 ch over 8 GPUs)"),
+}
+
+
+# --------------------------------------------------------------------------- harness
+def dist_env():
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def timed_loop(step, steps, warmup, sync, dist=None):
+    """W untimed steps, then K steps bracketed by barrier + sync on both sides.
+    Returns the elapsed seconds, maxed over ranks when `dist` is initialised."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(wl, sample_channels, procs):
+    """Times the CPU oracle chain on `sample_channels` channels with a fork pool."""
+    import multiprocessing as mp
+
+    import numpy as np
+
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(1)
+    xs = rng.uniform(-1, 1, (sample_channels, wl["n_in"])).astype(np.float32)
+    chunks = [xs[i::procs] for i in range(procs)]
+    args = [(list(c), wl["fs"], wl["L"], wl["M"], CONFIG3_GAINS, wl["num_taps"], wl["n_fft"])
+            for c in chunks if len(c)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(len(args)) as pool:
+        pool.map(orc.chain_batch_worker, [(a[0][:1],) + a[1:] for a in args])  # warm
+        t0 = time.perf_counter()
+        pool.map(orc.chain_batch_worker, args)
+        wall = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(sample_channels * wl["n_in"] / wall / 1e6, 4),
+        "unit": "Msamples/s",
+        "cores": len(args),
+        "kind": "port",
+        "sample": (f"{sample_channels} channels of the {wl['name']} chain (oracle/dsp_ref_cpu.py: "
+                   f"np.convolve SRC, scipy lfilter cascade, recursive radix-2 FFT), "
+                   f"{len(args)}-process pool, {wall:.2f} s wall, CPU: {cpu_model}"),
+    }
+
+
+# --------------------------------------------------------------------------- per-kernel bytes
+def kernel_bytes(chain, name):
+    """Algorithmic HBM bytes of one launch of kernel `name`."""
+    B, n_in, n_out = chain.B, chain.cfg.n_in, chain.n_out
+    T = chain.chunk_len
+    C = -(-n_out // T)
+    S = chain.sos.shape[0]
+    N = chain.spec.n_fft
+    return {
+        "src_poly": 4 * B * (n_in + n_out),
+        "iir_state": 4 * B * (C - 1) * T + 8 * 2 * S * B * (C - 1),
+        "iir_carry": 8 * 2 * S * B * (2 * C - 1),
+        "iir_apply": 8 * B * n_out + 8 * 2 * S * B * C,
+        "iir_prep": 8 * (2 * S) ** 2,
+        "spectrum": 4 * B * (chain.spec.seg_len + N // 2 + 1),
+    }.get(name, 0)
+
+
+def load_traffic(wl_name):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(wl_name, {})
+    except (OSError, ValueError):
+        return {}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--channels", type=int, default=None, help="channels per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=320,
+                    help="channels in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=16)
+    args = ap.parse_args(argv)
+
+    rank, local_rank, world = dist_env()
+    wl = dict(WORKLOADS[args.config])
+    if args.channels:
+        wl["channels"] = args.channels
+
+    # CPU baseline first: no GPU context exists yet when the pool forks.
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        procs = max(1, min(args.cpu_procs, os.cpu_count() or 1, args.cpu_sample))
+        cpu = cpu_baseline(wl, args.cpu_sample, procs)
+
+    import torch
+
+    from dspcore import _lib
+    from dspcore.chain import Chain, ChainConfig
+
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], CONFIG3_GAINS,
+                      n_fft=wl["n_fft"])
+    B = wl["channels"]
+    chain = Chain(cfg, B, device)
+    gen = torch.Generator(device=device).manual_seed(1000 + rank)
+    x = torch.rand((B, wl["n_in"]), generator=gen, device=device, dtype=torch.float32)
+    x.mul_(2).sub_(1)
+    torch.cuda.synchronize(device)
+
+    step = lambda: chain.run(x)  # noqa: E731
+    sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
+    elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
+    ms_per_step = elapsed / args.steps * 1e3
+    total_samples = B * wl["n_in"] * world * args.steps
+    value = total_samples / elapsed / 1e6
+
+    # Traced pass: HIP events around every launch, same stream as the kernels.
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    for _ in range(args.steps):
+        chain.run(x)
+    recs = _lib.trace_read()
+    _lib.trace_enable(False)
+    per = {}
+    for name, ms in recs:
+        per.setdefault(name, []).append(ms)
+    kernels = {k: round(sum(v) / len(v), 5) for k, v in per.items()}
+    dom = max(kernels, key=kernels.get)
+    dom_bytes = kernel_bytes(chain, dom)
+    achieved = dom_bytes / (kernels[dom] * 1e-3) / 1e9
+    traffic = load_traffic(wl["name"]).get(dom)
+    chain_bytes = chain.algorithmic_bytes()
+    chain_gbs = chain_bytes / (ms_per_step * 1e-3) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (IIR state/coefficients f64)",
+            "data": "synthetic uniform(-1,1) float32 generated on device (reference WAVs missing)",
+            "config": {
+                "workload": wl["desc"], "channels_per_gpu": B, "total_channels": B * world,
+                "n_in": wl["n_in"], "n_out": chain.n_out, "fs_in": wl["fs"],
+                "fs_out": chain.fs_out, "L": wl["L"], "M": wl["M"], "taps": chain.src.K,
+                "biquads": int(chain.sos.shape[0]), "n_fft": chain.spec.n_fft,
+                "parallelism": f"channel-shard x{world} (no collective)",
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "algorithmic_bytes": dom_bytes,
+                "mean_ms": kernels[dom],
+            },
+            "chain_roofline": {
+                "achieved": round(chain_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(chain_gbs / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_gpu_step": chain_bytes,
+            },
+            "kernels_ms": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+// extern "C" entry points of libdspcore.so (declared in include/dspcore.h).
+// Each one validates its arguments, launches on the caller's stream and
+// returns a status code; nothing throws across the ABI.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace dsp {
+
+namespace {
+thread_local std::string g_error;
+
+struct TraceRec {
+  const char* name;
+  hipEvent_t start, stop;
+};
+struct TraceState {
+  bool on = false;
+  std::vector<TraceRec> recs;  // recs[0..used) are live
+  size_t used = 0;
+};
+thread_local TraceState g_trace;
+}  // namespace
+
+TraceScope::TraceScope(const char* name, hipStream_t s) : slot_(-1), s_(s) {
+  TraceState& t = g_trace;
+  if (!t.on) return;
+  if (t.used == t.recs.size()) {
+    TraceRec r{name, nullptr, nullptr};
+    if (hipEventCreate(&r.start) != hipSuccess || hipEventCreate(&r.stop) != hipSuccess) return;
+    t.recs.push_back(r);
+  }
+  TraceRec& r = t.recs[t.used];
+  r.name = name;
+  if (hipEventRecord(r.start, s) != hipSuccess) return;
+  slot_ = (int)t.used++;
+}
+
+TraceScope::~TraceScope() {
+  if (slot_ >= 0) (void)hipEventRecord(g_trace.recs[slot_].stop, s_);
+}
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_error = buf;
+  return code;
+}
+
+void clear_error() { g_error.clear(); }
+
+}  // namespace dsp
+
+extern "C" {
+
+int dsp_version(void) { return 10000; /* 1.0.0 */ }
+
+const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
+
+int dsp_src_polyphase_f32(const float* x, float* y, int64_t B, int64_t n_in,
+                          int64_t ld_x, int64_t n_out, int64_t ld_y,
+                          const float* taps, int32_t K, int32_t L, int32_t M,
+                          int64_t c_offset, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
+                         static_cast<hipStream_t>(stream));
+}
+
+size_t dsp_biquad_workspace_bytes(int64_t B, int64_t n, int32_t S,
+                                  int64_t chunk_len) {
+  return dsp::biquad_workspace_bytes(B, n, S, chunk_len);
+}
+
+int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
+                           int64_t ld_x, int64_t ld_y, const double* sos_host,
+                           int32_t S, int32_t clip, int64_t chunk_len,
+                           void* workspace, size_t workspace_bytes,
+                           void* stream) {
+  dsp::clear_error();
+  return dsp::launch_biquad(x, y, B, n, ld_x, ld_y, sos_host, S, clip, chunk_len,
+                            workspace, workspace_bytes,
+                            static_cast<hipStream_t>(stream));
+}
+
+int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
+                       int32_t real_input, int64_t ld_in, int64_t ld_out,
+                       const float* twiddles, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_fft(in, out, B, log2n, real_input, ld_in, ld_out, twiddles,
+                         static_cast<hipStream_t>(stream));
+}
+
+int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
+                     int64_t seg_start, int64_t seg_len, int32_t log2n,
+                     int64_t ld_mag, const float* window,
+                     const float* twiddles, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_spectrum(x, mag, B, ld_x, seg_start, seg_len, log2n, ld_mag,
+                              window, twiddles, static_cast<hipStream_t>(stream));
+}
+
+int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
+                  int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
+                  const float* taps, int32_t K, int32_t L, int32_t M,
+                  int64_t c_offset, const double* sos_host, int32_t S,
+                  int32_t clip, int64_t chunk_len, int64_t seg_start,
+                  int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  const float* window, const float* twiddles, void* workspace,
+                  size_t workspace_bytes, void* stream) {
+  dsp::clear_error();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
+  int rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
+  if (rc) return rc;
+  rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
+                          workspace, workspace_bytes, s);
+  if (rc) return rc;
+  return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag,
+                              window, twiddles, s);
+}
+
+int dsp_trace_enable(int32_t enable) {
+  dsp::clear_error();
+  dsp::g_trace.on = enable != 0;
+  dsp::g_trace.used = 0;
+  return DSP_OK;
+}
+
+int dsp_trace_read(char* names, float* ms, int32_t max) {
+  dsp::clear_error();
+  auto& t = dsp::g_trace;
+  int n = 0;
+  for (size_t i = 0; i < t.used && n < max; ++i, ++n) {
+    const auto& r = t.recs[i];
+    DSP_HIP(hipEventSynchronize(r.stop));
+    float v = 0.f;
+    DSP_HIP(hipEventElapsedTime(&v, r.start, r.stop));
+    if (ms) ms[n] = v;
+    if (names) {
+      std::strncpy(names + (size_t)n * DSP_TRACE_NAME, r.name, DSP_TRACE_NAME - 1);
+      names[(size_t)n * DSP_TRACE_NAME + DSP_TRACE_NAME - 1] = 0;
+    }
+  }
+  t.used = 0;
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// Shared helpers for the libdspcore HIP sources (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "dspcore.h"
+
+namespace dsp {
+
+// Thread-local error string behind dsp_last_error(): every entry point is
+// reentrant and threads driving different GPUs never see each other's errors.
+int set_error(int code, const char* fmt, ...);
+void clear_error();
+
+#define DSP_REQUIRE(cond, ...)                              \
+  do {                                                      \
+    if (!(cond)) return ::dsp::set_error(DSP_EINVAL, __VA_ARGS__); \
+  } while (0)
+
+#define DSP_HIP(expr)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return ::dsp::set_error(DSP_EHIP, "%s failed: %s", #expr,              \
+                              hipGetErrorString(e_));                        \
+  } while (0)
+
+// Checks the launch that was just enqueued.
+#define DSP_LAUNCHED(name)                                                   \
+  do {                                                                       \
+    hipError_t e_ = hipGetLastError();                                       \
+    if (e_ != hipSuccess)                                                    \
+      return ::dsp::set_error(DSP_EHIP, "launch of %s failed: %s", name,     \
+                              hipGetErrorString(e_));                        \
+  } while (0)
+
+constexpr int kWave = 64;
+
+// RAII bracket of one kernel launch for dsp_trace_* (no-op unless enabled on
+// this thread).
+class TraceScope {
+ public:
+  TraceScope(const char* name, hipStream_t s);
+  ~TraceScope();
+  TraceScope(const TraceScope&) = delete;
+  TraceScope& operator=(const TraceScope&) = delete;
+
+ private:
+  int slot_;
+  hipStream_t s_;
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB).
+template <typename Kern>
+inline int allow_lds(Kern kernel, size_t bytes) {
+  if (bytes > 65536)
+    DSP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)bytes));
+  return DSP_OK;
+}
+
+// Internal launchers shared by the entry points and the fused chain.
+int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
+               int64_t n_out, int64_t ld_y, const float* taps, int K, int L,
+               int M, int64_t c, hipStream_t s);
+int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                  int64_t ld_y, const double* sos, int S, int clip,
+                  int64_t chunk_len, void* ws, size_t ws_bytes, hipStream_t s);
+int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
+                    int64_t seg_start, int64_t seg_len, int log2n,
+                    int64_t ld_mag, const float* window, const float* tw,
+                    hipStream_t s);
+int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
+               int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
+size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
+
+}  // namespace dsp

@@ -1,0 +1,242 @@
+// Polyphase L/M sample-rate converter for gfx950.
+//
+// Replaces reference modules/dsp_core.py:148-170: the expander (:149-150), the
+// 'same' convolution with L*h (:162,:166) and the decimator (:170).  The
+// reference computes N*L*K multiply-adds, (L-1)/L of them on inserted zeros,
+// then drops (M-1)/M of the outputs.  Here only the kept outputs are computed
+// and only the taps that meet a real input sample:
+//
+//   j = m*M + c, phi = j mod L, q = j div L
+//   y[m] = sum_t P[phi][t] * x[q - t],  P[phi][t] = taps[phi + L*t]
+//
+// i.e. ceil(K/L) FMAs per output.  Both kernels stage the block's input window
+// and the polyphase tap bank in LDS (coalesced, float4 where aligned) and
+// stream the outputs back through LDS as float4 stores.  HBM traffic is the
+// algorithmic minimum: x read once, y written once (window overlap between
+// neighbouring blocks is T-1 samples out of thousands).
+#include "common.h"
+
+namespace dsp {
+namespace {
+
+// Fills win[i] = x[qa + i] for i < nload (zeros outside [0, n_in)).
+// qa is a multiple of 4 so aligned rows allow float4 loads.
+template <int NT>
+__device__ __forceinline__ void load_window(float* __restrict__ win,
+                                            const float* __restrict__ xr,
+                                            int64_t qa, int nload, int64_t n_in,
+                                            bool vec_ok) {
+  const int nv = (nload + 3) >> 2;
+  for (int v = threadIdx.x; v < nv; v += NT) {
+    const int64_t q = qa + 4 * (int64_t)v;
+    float4 f;
+    if (vec_ok && q >= 0 && q + 3 < n_in) {
+      f = *reinterpret_cast<const float4*>(xr + q);
+    } else {
+      f.x = (q + 0 >= 0 && q + 0 < n_in) ? xr[q + 0] : 0.f;
+      f.y = (q + 1 >= 0 && q + 1 < n_in) ? xr[q + 1] : 0.f;
+      f.z = (q + 2 >= 0 && q + 2 < n_in) ? xr[q + 2] : 0.f;
+      f.w = (q + 3 >= 0 && q + 3 < n_in) ? xr[q + 3] : 0.f;
+    }
+    *reinterpret_cast<float4*>(win + 4 * v) = f;
+  }
+}
+
+// Writes out[0:count] to yr[0:count] (float4 when the row is aligned).
+template <int NT>
+__device__ __forceinline__ void store_tile(float* __restrict__ yr,
+                                           const float* __restrict__ out,
+                                           int count, bool vec_ok) {
+  if (vec_ok) {
+    const int nv = count >> 2;
+    for (int v = threadIdx.x; v < nv; v += NT)
+      *reinterpret_cast<float4*>(yr + 4 * v) =
+          *reinterpret_cast<const float4*>(out + 4 * v);
+    for (int i = 4 * nv + threadIdx.x; i < count; i += NT) yr[i] = out[i];
+  } else {
+    for (int i = threadIdx.x; i < count; i += NT) yr[i] = out[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Register-blocked kernel for a compile-time (L, M, T).
+// Thread (p, g) owns the R outputs m = m0 + p + g*L*R + r*L, r < R.  They share
+// one polyphase branch phi, and their input windows are shifted by M samples,
+// so one tap read feeds R FMAs and one window read feeds up to T FMAs:
+// (T + (R-1)M) + T LDS reads per R*T FMAs.
+// ---------------------------------------------------------------------------
+template <int L, int M, int T, int R, int NT>
+__global__ __launch_bounds__(NT) void k_src_reg(
+    const float* __restrict__ x, float* __restrict__ y, int64_t n_in,
+    int64_t ld_x, int64_t n_out, int64_t ld_y, const float* __restrict__ taps,
+    int K, int64_t c, int vec_x, int vec_y) {
+  constexpr int G = NT / L;          // thread groups with one thread per phase
+  constexpr int TILE = G * L * R;    // outputs per block
+  constexpr int TP = ((T + 3) / 4) * 4 + 4;               // padded bank row
+  constexpr int WMAX = ((TILE - 1) * M) / L + T + 2 + 8;  // window + align slack
+  static_assert(TILE % 4 == 0, "tile must be float4 aligned");
+
+  __shared__ __attribute__((aligned(16))) float s_bank[L * TP];
+  __shared__ __attribute__((aligned(16))) float s_win[((WMAX + 3) / 4) * 4];
+  __shared__ __attribute__((aligned(16))) float s_out[TILE];
+
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t m0 = (int64_t)blockIdx.x * TILE;
+  const float* xr = x + b * ld_x;
+  float* yr = y + b * ld_y;
+
+  const int64_t qlo = (m0 * M + c) / L - (T - 1);
+  const int64_t qhi = ((m0 + TILE - 1) * M + c) / L;
+  const int64_t qa = qlo & ~(int64_t)3;
+  load_window<NT>(s_win, xr, qa, (int)(qhi - qa + 1), n_in, vec_x != 0);
+
+  // Bank row phi holds the branch taps reversed: s_bank[phi][u] = P[phi][T-1-u].
+  for (int i = tid; i < L * TP; i += NT) {
+    const int phi = i / TP, u = i - phi * TP;
+    const int k = phi + L * (T - 1 - u);
+    s_bank[i] = (u < T && k < K) ? taps[k] : 0.f;
+  }
+  __syncthreads();
+
+  if (tid < G * L) {
+    const int p = tid % L, g = tid / L;
+    const int lbase = p + g * L * R;                 // local index of r = 0
+    const int64_t j = (m0 + lbase) * M + c;
+    const int64_t q = j / L;
+    const int phi = (int)(j - q * L);
+    const float* w = s_win + (int)(q - (T - 1) - qa);
+    const float* h = s_bank + phi * TP;
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      const float t = h[u];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = fmaf(t, w[r * M + u], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r];
+  }
+  __syncthreads();
+
+  const int64_t count = min((int64_t)TILE, n_out - m0);
+  store_tile<NT>(yr + m0, s_out, (int)count, vec_y != 0);
+}
+
+// ---------------------------------------------------------------------------
+// Generic kernel: any L, M, K.  One output per thread-iteration, T taps each.
+// LDS: tap bank [L][T] + input window, both carved from dynamic LDS.
+// ---------------------------------------------------------------------------
+constexpr int kGenNT = 256;
+constexpr int kGenTile = 1024;
+
+__global__ __launch_bounds__(kGenNT) void k_src_generic(
+    const float* __restrict__ x, float* __restrict__ y, int64_t n_in,
+    int64_t ld_x, int64_t n_out, int64_t ld_y, const float* __restrict__ taps,
+    int K, int L, int M, int T, int64_t c, int tile, int bank_floats,
+    int vec_x, int vec_y) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_bank = smem;                       // [L][T], bank_floats (mult. of 4)
+  float* s_win = smem + bank_floats;          // window
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t m0 = (int64_t)blockIdx.x * tile;
+  const int64_t m1 = min(m0 + tile, n_out);
+  const float* xr = x + b * ld_x;
+  float* yr = y + b * ld_y;
+
+  const int64_t qlo = (m0 * M + c) / L - (T - 1);
+  const int64_t qhi = ((m1 - 1) * M + c) / L;
+  const int64_t qa = qlo & ~(int64_t)3;
+  load_window<kGenNT>(s_win, xr, qa, (int)(qhi - qa + 1), n_in, vec_x != 0);
+  for (int i = tid; i < L * T; i += kGenNT) {
+    const int phi = i / T, u = i - phi * T;
+    const int k = phi + L * (T - 1 - u);
+    s_bank[i] = (k < K) ? taps[k] : 0.f;
+  }
+  __syncthreads();
+
+  // Output stores are coalesced directly (consecutive threads, consecutive m).
+  (void)vec_y;
+  for (int64_t m = m0 + tid; m < m1; m += kGenNT) {
+    const int64_t j = m * M + c;
+    const int64_t q = j / L;
+    const int phi = (int)(j - q * L);
+    const float* w = s_win + (int)(q - (T - 1) - qa);
+    const float* h = s_bank + phi * T;
+    float a0 = 0.f, a1 = 0.f;
+    int u = 0;
+    for (; u + 1 < T; u += 2) {
+      a0 = fmaf(h[u], w[u], a0);
+      a1 = fmaf(h[u + 1], w[u + 1], a1);
+    }
+    if (u < T) a0 = fmaf(h[u], w[u], a0);
+    yr[m] = a0 + a1;
+  }
+}
+
+template <int L, int M, int T, int R, int NT>
+int run_reg(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
+            int64_t n_out, int64_t ld_y, const float* taps, int K, int64_t c,
+            int vec_x, int vec_y, hipStream_t s) {
+  constexpr int TILE = (NT / L) * L * R;
+  dim3 grid((unsigned)ceil_div(n_out, TILE), (unsigned)B);
+  TraceScope trace("src_poly", s);
+  hipLaunchKernelGGL((k_src_reg<L, M, T, R, NT>), grid, dim3(NT), 0, s, x, y,
+                     n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y);
+  DSP_LAUNCHED("k_src_reg");
+  return DSP_OK;
+}
+
+}  // namespace
+
+int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
+               int64_t n_out, int64_t ld_y, const float* taps, int K, int L,
+               int M, int64_t c, hipStream_t s) {
+  DSP_REQUIRE(B >= 0 && n_in >= 1 && n_out >= 0, "bad sizes B=%lld n_in=%lld n_out=%lld",
+              (long long)B, (long long)n_in, (long long)n_out);
+  DSP_REQUIRE(L >= 1 && M >= 1 && K >= 1, "bad L=%d M=%d K=%d", L, M, K);
+  DSP_REQUIRE(c >= 0, "bad c_offset %lld", (long long)c);
+  DSP_REQUIRE(ld_x >= n_in && ld_y >= n_out, "leading dimension too small");
+  DSP_REQUIRE(B <= 65535, "B=%lld exceeds the grid's y extent (65535); split the batch",
+              (long long)B);
+  if (B == 0 || n_out == 0) return DSP_OK;
+  DSP_REQUIRE(x && y && taps, "null pointer");
+  const int T = (K + L - 1) / L;
+  const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
+
+  // Register-blocked instantiations: the benchmark configurations and the
+  // app's most common (L, M) pairs with the default tap rule 40*max(L,M)+1.
+  if (L == 3 && M == 2 && T == 41)
+    return run_reg<3, 2, 41, 16, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+  if (L == 3 && M == 2 && T == 85)
+    return run_reg<3, 2, 85, 8, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+  if (L == 2 && M == 1 && T == 64)
+    return run_reg<2, 1, 64, 16, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+  if (L == 2 && M == 1 && T == 41)
+    return run_reg<2, 1, 41, 16, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+
+  // Generic path.  Shrink the tile until bank + window fit in LDS.
+  const int bank_floats = ((L * T + 3) / 4) * 4;
+  int tile = kGenTile;
+  auto lds_bytes = [&](int t) {
+    const int64_t w = ((int64_t)(t - 1) * M) / L + T + 2 + 8;
+    return (int64_t)(bank_floats + ((w + 3) / 4) * 4) * 4;
+  };
+  while (tile > 64 && lds_bytes(tile) > 160 * 1024) tile >>= 1;
+  if (lds_bytes(tile) > 160 * 1024)
+    return set_error(DSP_ENOTSUP, "tap bank L*ceil(K/L)=%d floats does not fit in LDS", L * T);
+  dim3 grid((unsigned)ceil_div(n_out, tile), (unsigned)B);
+  const size_t shm = (size_t)lds_bytes(tile);
+  if (int rc = allow_lds(k_src_generic, shm)) return rc;
+  TraceScope trace("src_poly", s);
+  hipLaunchKernelGGL(k_src_generic, grid, dim3(kGenNT), shm, s, x, y, n_in, ld_x,
+                     n_out, ld_y, taps, K, L, M, T, c, tile, bank_floats, vec_x, vec_y);
+  DSP_LAUNCHED("k_src_generic");
+  return DSP_OK;
+}
+
+}  // namespace dsp

@@ -1,0 +1,124 @@
+"""Batched SRC -> EQ -> spectrum chain: the hot path of app.py:164-167 and
+app.py:203-205 for B channels at once, planned once and replayed.
+
+A Chain owns every device buffer (taps, LUTs, y, z, mag, workspace) so that
+`run()` is only kernel launches: graph-capturable, no allocation, no sync.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from .design import EqPlan, SpectrumPlan, SrcPlan, eq_plan, spectrum_plan, src_plan
+
+
+@dataclass(frozen=True)
+class ChainConfig:
+    n_in: int
+    fs: int
+    L: int
+    M: int
+    num_taps: int | None
+    gains: dict
+    n_fft: int = 2048
+    limit_pts: int | None = None     # app.py:202 spectra use sig[:100000]
+
+
+class Chain:
+    """Device-resident plan of the chain for a fixed batch size."""
+
+    def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
+                 chunk_len: int = ops.CHUNK_LEN):
+        ops.require_gpu()
+        self.cfg = cfg
+        self.B = int(batch)
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.src: SrcPlan = src_plan(cfg.n_in, cfg.fs, cfg.M, cfg.L, cfg.num_taps)
+        self.identity_src = cfg.L == 1 and cfg.M == 1
+        n_out = cfg.n_in if self.identity_src else self.src.n_out
+        self.n_out = n_out
+        self.fs_out = cfg.fs if self.identity_src else self.src.fs_out
+        self.eq: EqPlan = eq_plan(self.fs_out, cfg.gains)
+        spec_len = n_out if cfg.limit_pts is None else min(n_out, cfg.limit_pts)
+        self.spec: SpectrumPlan = spectrum_plan(spec_len, cfg.n_fft)
+        self.chunk_len = int(chunk_len)
+        dev = self.device
+        self.taps = ops.taps_tensor(self.src, dev)
+        self.window = ops._table("hann", self.spec.n_fft, dev)
+        self.tw = ops._table("tw", self.spec.n_fft, dev)
+        self.sos = np.ascontiguousarray(self.eq.sos, dtype=np.float64)
+        self.y = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
+        self.z = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
+        self.mag = torch.empty((self.B, self.spec.n_fft // 2 + 1), dtype=torch.float32,
+                               device=dev)
+        self.workspace = ops.biquad_workspace(self.B, n_out, self.sos.shape[0], dev,
+                                              self.chunk_len)
+
+    # -- algorithmic traffic ---------------------------------
+    def algorithmic_bytes(self) -> int:
+        """4*N_in + 4*N_out (y) + 4*N_out (z) + 4*(N/2+1) per channel."""
+        per = 4 * self.cfg.n_in + 8 * self.n_out + 4 * (self.spec.n_fft // 2 + 1)
+        return per * self.B
+
+    def check_input(self, x: torch.Tensor) -> torch.Tensor:
+        if x.shape != (self.B, self.cfg.n_in) or x.dtype != torch.float32 or not x.is_cuda:
+            raise ValueError(f"expected float32 CUDA [{self.B}, {self.cfg.n_in}], got "
+                             f"{x.dtype} {tuple(x.shape)}")
+        if x.stride(1) != 1:
+            x = x.contiguous()
+        return x
+
+    def run(self, x: torch.Tensor):
+        """One fused-call pass: y = SRC(x), z = EQ(y), mag = |FFT(hann*z[seg])|."""
+        x = self.check_input(x)
+        if self.identity_src:
+            # SRC bypass (dsp_core.py:144-145): y is x itself.
+            self.run_stages(x)
+            return x, self.z, self.mag
+        lib = _lib.load()
+        sos_ptr = _lib.sos_pointer(self.sos)
+        S = self.sos.shape[0]
+        clip = 0 if self.eq.bypass else 1
+        with torch.cuda.device(self.device):
+            rc = lib.dsp_chain_f32(
+                x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.mag.data_ptr(),
+                self.B, self.cfg.n_in, x.stride(0), self.n_out, self.y.stride(0),
+                self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
+                sos_ptr, S, clip, self.chunk_len, self.spec.seg_start, self.spec.seg_len,
+                self.spec.n_fft.bit_length() - 1, self.mag.stride(0),
+                self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
+                self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(rc, "dsp_chain_f32")
+        return self.y, self.z, self.mag
+
+    def run_stages(self, x: torch.Tensor, events: list | None = None):
+        """Same pass, one entry point per stage; optional (start, end) event pairs
+        around each stage for per-kernel timing on the current stream."""
+        x = self.check_input(x)
+
+        def mark(i, which):
+            if events is not None:
+                events[i][which].record()
+
+        mark(0, 0)
+        if self.identity_src:
+            y = x
+        else:
+            y = ops.src_polyphase(x, self.src, self.taps, out=self.y)
+        mark(0, 1)
+        mark(1, 0)
+        if self.eq.bypass:
+            z = y                       # dsp_core.py:222-223 returns its input
+        else:
+            z = ops.biquad_cascade(y, self.sos, True, out=self.z, workspace=self.workspace,
+                                   chunk_len=self.chunk_len)
+        mark(1, 1)
+        mark(2, 0)
+        ops.spectrum(z, self.spec.seg_start, self.spec.seg_len, self.spec.n_fft, out=self.mag)
+        mark(2, 1)
+        return y, z, self.mag

@@ -1,0 +1,200 @@
+"""Host-side filter design and call planning (float64, numpy).
+
+These are the parts of reference modules/dsp_core.py that run once per call
+and are O(taps) or O(bands): the FIR designer, the peaking-biquad designer,
+the EQ band selection and the SRC / spectrum size rules.  They stay on the host
+in float64 exactly as the reference computes them; only their results (fp32
+taps, fp64 second-order sections, sizes) cross into the HIP kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+# Band centres of the 6-band EQ, in the reference's order
+# (reference modules/dsp_core.py:225-228).
+BAND_CENTRES_HZ = {
+    "Sub-Bass": 40, "Bass": 150, "Low Mids": 1000,
+    "High Mids": 3000, "Presence": 5000, "Brilliance": 10000,
+}
+DEFAULT_CENTRE_HZ = 1000      # unknown band name (dsp_core.py:235)
+BYPASS_DB = 0.1               # |g| threshold (dsp_core.py:222, :234)
+NYQUIST_FRACTION = 0.90       # fc ceiling = 0.9 * fs/2 (dsp_core.py:240)
+MIN_CENTRE_HZ = 10            # fc floor (dsp_core.py:249)
+SPECTRUM_WINDOW = 2048        # N_ventana (dsp_core.py:74)
+
+
+def sinc_lowpass(w_c_norm: float, num_taps: int) -> np.ndarray:
+    """Windowed-sinc low-pass, unit DC gain (reference dsp_core.py:104-131).
+
+    An even tap count is bumped to odd (:114); taps are sinc(wc*n), n centred on
+    0 (:116-120), times a Blackman window (:123-124), normalised to sum 1 when
+    the sum is non-zero (:127-129).
+    """
+    k = int(num_taps) + (1 - int(num_taps) % 2)
+    half = k // 2
+    n = np.arange(-half, half + 1)
+    h = np.sinc(w_c_norm * n) * np.blackman(n.size)
+    total = np.sum(h)
+    if total != 0:
+        h /= total
+    return h
+
+
+def default_num_taps(L: int, M: int) -> int:
+    """Tap rule of dsp_core.py:158: 40 * max(L, M) + 1."""
+    return 40 * max(L, M) + 1
+
+
+@dataclass(frozen=True)
+class SrcPlan:
+    """Sizes and taps of one polyphase SRC call (dsp_core.py:133-173)."""
+    L: int
+    M: int
+    K: int                 # odd tap count actually used
+    taps: np.ndarray       # float64 L*h, length K
+    c_offset: int          # 'same' centring offset into the full convolution
+    n_in: int
+    n_out: int
+    fs_out: int
+
+
+def src_plan(n_in: int, fs: int, M: int, L: int, num_taps: int | None = None) -> SrcPlan:
+    """Plans conversion_tasa_muestreo(x, fs, M, L) for a signal of n_in samples.
+
+    wc = 1/max(L, M) (:155); K from `num_taps` or the default rule (:158);
+    h *= L (:162).  np.convolve(x_e, h, 'same') keeps max(NL, K) samples of the
+    full convolution starting at c = (min(NL, K) - 1) // 2 (:166); [::M] keeps
+    ceil(max(NL, K) / M) of them (:170); fs' = int(fs * L / M) (:172).
+    """
+    L, M = int(L), int(M)
+    if L < 1 or M < 1:
+        raise ValueError(f"L and M must be >= 1 (got L={L}, M={M})")
+    if n_in < 1:
+        raise ValueError("conversion_tasa_muestreo needs at least one sample")
+    taps_req = default_num_taps(L, M) if num_taps is None else int(num_taps)
+    h = sinc_lowpass(1.0 / max(L, M), taps_req)
+    h *= L
+    K = h.size
+    nl = n_in * L
+    c = (min(nl, K) - 1) // 2
+    n_out = -(-max(nl, K) // M)
+    return SrcPlan(L, M, K, h, c, n_in, n_out, int(fs * L / M))
+
+
+def peaking_biquad(fc: float, fs: float, gain_db: float) -> tuple[np.ndarray, np.ndarray]:
+    """RBJ-style peaking EQ with Q = 1 (reference dsp_core.py:179-203).
+
+    Returns (b, a), both float64[3] normalised so a[0] == 1.
+    """
+    w0 = 2 * np.pi * fc / fs
+    alpha = np.sin(w0) / 2.0
+    amp = 10 ** (gain_db / 40.0)
+    cosw = np.cos(w0)
+    a0 = 1 + alpha / amp
+    b = np.array([1 + alpha * amp, -2 * cosw, 1 - alpha * amp]) / a0
+    a = np.array([a0, -2 * cosw, 1 - alpha / amp]) / a0
+    return b, a
+
+
+@dataclass(frozen=True)
+class EqPlan:
+    """What sistema_ecualizador does for given (fs, gains) (dsp_core.py:216-254)."""
+    bypass: bool           # all |g| < 0.1: the input object is returned as is
+    sos: np.ndarray        # float64 [S][5] = b0 b1 b2 a1 a2, in dict order
+    centres: tuple         # effective fc of each stage (after the clamp)
+
+
+def eq_plan(fs: float, gains: dict) -> EqPlan:
+    """Band selection of dsp_core.py:222-251.
+
+    Bypass when every |g| < 0.1 (an empty dict bypasses too).  Otherwise, in
+    dict order, every band with |g| > 0.1 gets fc from the centre table (1000 Hz
+    for an unknown name), clamped to 0.9*fs/2 when fc >= that ceiling, and is
+    applied only if fc > 10 Hz.  The clip to [-1, 1] always follows.
+    """
+    values = list(gains.values())
+    if all(abs(g) < BYPASS_DB for g in values):
+        return EqPlan(True, np.zeros((0, 5)), ())
+    ceiling = (fs / 2.0) * NYQUIST_FRACTION
+    rows, centres = [], []
+    for name, g in gains.items():
+        if not abs(g) > BYPASS_DB:
+            continue
+        fc = BAND_CENTRES_HZ.get(name, DEFAULT_CENTRE_HZ)
+        if fc >= ceiling:
+            fc = ceiling
+        if fc > MIN_CENTRE_HZ:
+            b, a = peaking_biquad(fc, fs, g)
+            rows.append([b[0], b[1], b[2], a[1], a[2]])
+            centres.append(fc)
+    sos = np.asarray(rows, dtype=np.float64).reshape(-1, 5)
+    return EqPlan(False, sos, tuple(centres))
+
+
+def tf_to_sos_row(b, a) -> np.ndarray:
+    """(b, a) of order <= 2 -> one normalised DF2T row {b0 b1 b2 a1 a2}.
+
+    lfilter divides every coefficient by a[0]; shorter vectors are zero-padded.
+    """
+    b = np.atleast_1d(np.asarray(b, dtype=np.float64))
+    a = np.atleast_1d(np.asarray(a, dtype=np.float64))
+    if b.ndim != 1 or a.ndim != 1 or b.size == 0 or a.size == 0:
+        raise ValueError("b and a must be non-empty 1-D coefficient vectors")
+    if b.size > 3 or a.size > 3:
+        raise ValueError("the GPU cascade takes biquads: len(b), len(a) <= 3")
+    if a[0] == 0:
+        raise ValueError("BUG: filter coefficient a[0] == 0 not supported yet")
+    bb = np.zeros(3)
+    aa = np.zeros(3)
+    bb[: b.size] = b
+    aa[: a.size] = a
+    bb /= aa[0]
+    aa /= aa[0]
+    return np.array([bb[0], bb[1], bb[2], aa[1], aa[2]])
+
+
+@dataclass(frozen=True)
+class SpectrumPlan:
+    seg_start: int
+    seg_len: int
+    n_fft: int             # transform length actually used (power of two)
+
+
+def spectrum_plan(length: int, window: int = SPECTRUM_WINDOW) -> SpectrumPlan:
+    """Segment rule of calcular_espectro_magnitud (dsp_core.py:74-82).
+
+    len > window: x[len//2 : len//2 + window] (numpy slicing may truncate it);
+    otherwise zero-pad to the next power of two of len.  The reference's FFT
+    only works on power-of-two lengths, so a truncated segment whose length is
+    not a power of two raises ValueError exactly where the reference does
+    (e.g. 2048 < len < 4095 with the default window).
+    """
+    length = int(length)
+    if length > window:
+        start = length // 2
+        seg = min(window, length - start)
+        n = seg
+    else:
+        start = 0
+        seg = length
+        n = 1 << (length - 1).bit_length()
+    if n & (n - 1):
+        raise ValueError(
+            f"segment of {n} samples is not a power of two "
+            f"(signal length {length}, window {window}); the radix-2 FFT needs 2^k points")
+    return SpectrumPlan(start, seg, n)
+
+
+def hann(n: int) -> np.ndarray:
+    """Window of dsp_core.py:85-87: 0.5 - 0.5 cos(2 pi n / (N - 1)), float64."""
+    k = np.arange(n)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return 0.5 - 0.5 * np.cos(2 * np.pi * k / (n - 1))
+
+
+def twiddles(n: int) -> np.ndarray:
+    """exp(-2j pi k / N), k < N/2, computed in float64 (dsp_core.py:59-60)."""
+    k = np.arange(max(n // 2, 1))
+    return np.exp(-2j * np.pi * k / n)

@@ -1,0 +1,173 @@
+"""Device-level operators: torch CUDA tensors in, torch CUDA tensors out.
+
+Each function launches the matching libdspcore entry point on the current
+torch stream of the tensor's device and returns without synchronising.  The
+tensors are only device buffers (PyTorch-ROCm plumbing); all arithmetic is in
+the hand-written HIP kernels.  Layout: row-major [B, n] float32 (complex64 for
+FFT data), one row per audio channel.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+from .design import SrcPlan, hann, twiddles
+
+# Chunk length of the biquad carry scan.  Fixed (not derived from the batch)
+# so every row's result is bitwise independent of batch size and sharding.
+CHUNK_LEN = 2048
+
+_tables_lock = threading.Lock()
+_tables: dict = {}
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "dspcore needs a ROCm GPU (MI355X/gfx950): torch.cuda.is_available() is False; "
+            "there is no CPU fallback")
+    _lib.load()
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _table(kind: str, n: int, device: torch.device) -> torch.Tensor:
+    """Cached per-device LUTs: Hann window (fp32[n]) and twiddles (fp32[2*(n/2)])."""
+    key = (kind, n, device.index)
+    t = _tables.get(key)
+    if t is None:
+        with _tables_lock:
+            t = _tables.get(key)
+            if t is None:
+                if kind == "hann":
+                    host = hann(n).astype(np.float32)
+                else:
+                    host = twiddles(n).astype(np.complex64).view(np.float32)
+                t = torch.from_numpy(np.ascontiguousarray(host)).to(device)
+                _tables[key] = t
+    return t
+
+
+def _rows(x: torch.Tensor, name: str) -> torch.Tensor:
+    if not x.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (ROCm) tensor")
+    if x.dim() != 2:
+        raise ValueError(f"{name} must be [B, n], got shape {tuple(x.shape)}")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    return x
+
+
+def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:
+    return torch.from_numpy(plan.taps.astype(np.float32)).to(device)
+
+
+def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = None,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = SRC(x) for every row (dsp_core.py:148-170), fp32."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    B, n_in = x.shape
+    if n_in != plan.n_in:
+        raise ValueError(f"plan is for n_in={plan.n_in}, got {n_in}")
+    if taps is None:
+        taps = taps_tensor(plan, x.device)
+    if out is None:
+        out = torch.empty((B, plan.n_out), dtype=torch.float32, device=x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_src_polyphase_f32(
+            _ptr(x), _ptr(out), B, n_in, x.stride(0), plan.n_out, out.stride(0),
+            _ptr(taps), plan.K, plan.L, plan.M, plan.c_offset, _stream(x.device))
+    _lib.check(rc, "dsp_src_polyphase_f32")
+    return out
+
+
+def biquad_workspace(B: int, n: int, S: int, device: torch.device,
+                     chunk_len: int = CHUNK_LEN) -> torch.Tensor:
+    nbytes = _lib.load().dsp_biquad_workspace_bytes(B, n, S, chunk_len)
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
+                   out: torch.Tensor | None = None, workspace: torch.Tensor | None = None,
+                   chunk_len: int = CHUNK_LEN) -> torch.Tensor:
+    """z = clip(cascade(x)) per row (dsp_core.py:233-254), fp64 inside, fp32 I/O."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    sos = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 5)
+    B, n = x.shape
+    S = sos.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    if workspace is None:
+        workspace = biquad_workspace(B, n, S, x.device, chunk_len)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_biquad_cascade_f32(
+            _ptr(x), _ptr(out), B, n, x.stride(0), out.stride(0), _lib.sos_pointer(sos),
+            S, int(bool(clip)), chunk_len, _ptr(workspace), workspace.numel(),
+            _stream(x.device))
+    _lib.check(rc, "dsp_biquad_cascade_f32")
+    return out
+
+
+def _log2(n: int) -> int:
+    if n < 1 or n & (n - 1):
+        raise ValueError(f"length {n} is not a power of two; the radix-2 FFT needs 2^k points")
+    lg = n.bit_length() - 1
+    if lg > _lib.DSP_MAX_LOG2N:
+        raise RuntimeError(f"FFT length 2^{lg} exceeds the LDS-resident limit 2^{_lib.DSP_MAX_LOG2N}")
+    return lg
+
+
+def fft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Natural-order radix-2 DIT FFT of every row (dsp_core.py:41-66), complex64."""
+    x = _rows(x, "x")
+    B, n = x.shape
+    lg = _log2(n)
+    real = not x.is_complex()
+    if real:
+        x = x.float()
+    elif x.dtype != torch.complex64:
+        x = x.to(torch.complex64)
+    if out is None:
+        out = torch.empty((B, n), dtype=torch.complex64, device=x.device)
+    tw = _table("tw", n, x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_fft_r2_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), x.stride(0),
+                                    out.stride(0), _ptr(tw), _stream(x.device))
+    _lib.check(rc, "dsp_fft_r2_c2c_f32")
+    return out
+
+
+def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """|FFT(hann * x[seg])|[:n_fft/2+1] per row (dsp_core.py:74-98), fp32."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    B = x.shape[0]
+    lg = _log2(n_fft)
+    if out is None:
+        out = torch.empty((B, n_fft // 2 + 1), dtype=torch.float32, device=x.device)
+    win = _table("hann", n_fft, x.device)
+    tw = _table("tw", n_fft, x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_spectrum_f32(_ptr(x), _ptr(out), B, x.stride(0), seg_start, seg_len,
+                                  lg, out.stride(0), _ptr(win), _ptr(tw), _stream(x.device))
+    _lib.check(rc, "dsp_spectrum_f32")
+    return out

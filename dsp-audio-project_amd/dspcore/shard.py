@@ -1,0 +1,60 @@
+"""Multi-GPU shard driver for the channel batch.
+
+Channels never interact, so a batch is cut into contiguous channel ranges of
+ceil(B/g) rows, one per device; each device gets its own copy of the LUTs and
+runs the same kernels on its own stream from its own host thread (ctypes drops
+the GIL while the ABI runs).  No collective, no device-to-device traffic: the
+per-device results are gathered on the host.  Because the kernels' results do
+not depend on the batch size, the output is bitwise identical for any g.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import torch
+
+
+def shard_ranges(B: int, parts: int) -> list[tuple[int, int]]:
+    """Contiguous [lo, hi) ranges of ceil(B/parts) rows (the last may be short;
+    trailing empty ranges are dropped)."""
+    if parts < 1:
+        raise ValueError("parts must be >= 1")
+    step = -(-B // parts) if B else 0
+    out = []
+    for p in range(parts):
+        lo, hi = p * step, min(B, (p + 1) * step)
+        if lo < hi:
+            out.append((lo, hi))
+    return out
+
+
+def run_sharded(fn, x: np.ndarray, devices: list | None = None) -> list:
+    """Applies fn(x_dev) -> tuple of CUDA tensors to each shard of x's rows on its
+    own device and returns the tuple of host arrays concatenated along rows.
+
+    fn runs inside `torch.cuda.device(dev)` on that device's current stream."""
+    if devices is None:
+        devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    ranges = shard_ranges(x.shape[0], len(devices))
+    results: list = [None] * len(ranges)
+    errors: list = []
+
+    def worker(i, dev, lo, hi):
+        try:
+            with torch.cuda.device(dev):
+                xd = torch.from_numpy(np.ascontiguousarray(x[lo:hi], dtype=np.float32)).to(dev)
+                outs = fn(xd)
+                results[i] = tuple(o.cpu().numpy() for o in outs)
+        except BaseException as e:  # re-raised on the caller's thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(i, devices[i], lo, hi))
+               for i, (lo, hi) in enumerate(ranges)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return [np.concatenate([r[k] for r in results], axis=0) for k in range(len(results[0]))]

@@ -1,0 +1,141 @@
+/*
+ * dspcore.h — C-ABI of libdspcore.so, the MI355X (gfx950) hot path of
+ * Renatovela-ctrl/dsp-audio-project's modules/dsp_core.py.
+ *
+ * The reference has no native code and no FFI: its "operator API" is the set of
+ * module-level Python functions in modules/dsp_core.py.  Each entry point below
+ * replaces the numeric inner loop of one of them; the Python drop-in
+ * (dsp-audio-project_amd/modules/dsp_core.py) keeps the reference signatures and
+ * binds these symbols with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - every data pointer is a DEVICE pointer owned by the caller; the library
+ *     never allocates device memory.  Scratch space comes from the caller via
+ *     `workspace` (size from the matching *_workspace_bytes query);
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); every launch is
+ *     asynchronous on it, nothing synchronises, so calls are graph-capturable;
+ *   - kernels run on the calling thread's current HIP device;
+ *   - batches are row-major [B][ld] float32 (complex data interleaved re,im);
+ *   - return 0 (DSP_OK) on success, a negative DSP_E* code otherwise; the
+ *     thread-local dsp_last_error() string says why.  Nothing throws across
+ *     the ABI and no global mutable state is shared between threads.
+ */
+#ifndef DSPCORE_H
+#define DSPCORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSP_OK 0
+#define DSP_EINVAL (-1)   /* invalid argument: maps to Python ValueError      */
+#define DSP_EHIP (-2)     /* HIP runtime error: maps to Python RuntimeError   */
+#define DSP_ENOTSUP (-3)  /* valid but unsupported size: RuntimeError         */
+
+#define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
+#define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
+
+/* ABI version (major*10000 + minor*100 + patch). */
+int dsp_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* dsp_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Sample-rate conversion, polyphase L/M.
+ * Replaces dsp_core.py:148-170 (conversion_tasa_muestreo): zero-stuff by L
+ * (:149-150), np.convolve(x_e, h*L, mode='same') (:162,:166), keep every M-th
+ * sample (:170).  For every output m < n_out:
+ *     j = m*M + c_offset,  phi = j mod L,  q = j div L
+ *     y[m] = sum_{t >= 0, phi + L t < K} taps[phi + L t] * x[q - t]
+ * with x == 0 outside [0, n_in).  `taps` are the K gain-compensated filter
+ * coefficients L*h (dsp_core.py:159-162) already rounded to float32,
+ * c_offset = (min(n_in*L, K) - 1) / 2 ('same' centring),
+ * n_out = ceil(max(n_in*L, K) / M).  Accumulation is float32.
+ * ------------------------------------------------------------------------- */
+int dsp_src_polyphase_f32(const float* x, float* y, int64_t B, int64_t n_in,
+                          int64_t ld_x, int64_t n_out, int64_t ld_y,
+                          const float* taps, int32_t K, int32_t L, int32_t M,
+                          int64_t c_offset, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Biquad cascade (direct form II transposed), zero initial state.
+ * Replaces dsp_core.py:233-254 (sistema_ecualizador's serial loop of
+ * aplicar_ecuacion_diferencias = scipy.signal.lfilter, dsp_core.py:205-214,
+ * then np.clip(y, -1, 1) when clip != 0).
+ * `sos_host` is a HOST array [S][5] = {b0, b1, b2, a1, a2} per stage, a0 == 1,
+ * float64; coefficients and state are float64 inside the kernel, I/O float32.
+ * The time axis is cut into chunks of `chunk_len` samples (multiple of 32)
+ * whose initial states are recovered by a linear-recurrence carry pass, so
+ * results do not depend on B or on how a batch is sharded.  x may equal y.
+ * ------------------------------------------------------------------------- */
+size_t dsp_biquad_workspace_bytes(int64_t B, int64_t n, int32_t S,
+                                  int64_t chunk_len);
+int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
+                           int64_t ld_x, int64_t ld_y, const double* sos_host,
+                           int32_t S, int32_t clip, int64_t chunk_len,
+                           void* workspace, size_t workspace_bytes,
+                           void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Radix-2 decimation-in-time FFT, batched, natural-order output.
+ * Replaces dsp_core.py:41-66 (fft_diezmado_en_tiempo).  N = 2^log2n,
+ * 0 <= log2n <= DSP_MAX_LOG2N.  real_input != 0: `in` is float32 [B][ld_in]
+ * real samples; otherwise interleaved complex [B][ld_in] (ld in complex
+ * elements).  `out` is interleaved complex [B][ld_out].  `twiddles` is the
+ * interleaved complex table exp(-2*pi*i*k/N), k < N/2, in float32.
+ * ------------------------------------------------------------------------- */
+int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
+                       int32_t real_input, int64_t ld_in, int64_t ld_out,
+                       const float* twiddles, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Windowed magnitude spectrum of one segment per row.
+ * Replaces dsp_core.py:74-98 (calcular_espectro_magnitud): segment
+ * x[seg_start : seg_start + seg_len] zero-padded to N = 2^log2n (:76-82),
+ * times window[N] (Hann, :85-87), FFT (:90), |X[k]| for k <= N/2 (:91,:97-98).
+ * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.
+ * ------------------------------------------------------------------------- */
+int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
+                     int64_t seg_start, int64_t seg_len, int32_t log2n,
+                     int64_t ld_mag, const float* window,
+                     const float* twiddles, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Whole hot path of app.py:164-167 + :203-205 for a batch of channels:
+ *   y   = SRC(x)                     (dsp_src_polyphase_f32)
+ *   z   = clip(cascade(y))           (dsp_biquad_cascade_f32; S == 0 and
+ *                                     clip == 0 is the EQ bypass: z := y)
+ *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
+ * y and z must not alias.  workspace_bytes >= dsp_biquad_workspace_bytes().
+ * ------------------------------------------------------------------------- */
+int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
+                  int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
+                  const float* taps, int32_t K, int32_t L, int32_t M,
+                  int64_t c_offset, const double* sos_host, int32_t S,
+                  int32_t clip, int64_t chunk_len, int64_t seg_start,
+                  int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  const float* window, const float* twiddles, void* workspace,
+                  size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Per-launch tracing (the reference has no tracing; this is the build's).
+ * While enabled on the calling thread, every kernel this thread launches
+ * through the library is bracketed by two hipEventRecord calls on its stream
+ * (events are created once and reused).  dsp_trace_read waits for the
+ * recorded events, copies up to `max` records (name: NUL-terminated, stride
+ * DSP_TRACE_NAME bytes; duration in milliseconds) and clears the list; it
+ * returns the number of records copied or a negative DSP_E* code.
+ * ------------------------------------------------------------------------- */
+#define DSP_TRACE_NAME 32
+int dsp_trace_enable(int32_t enable);
+int dsp_trace_read(char* names, float* ms, int32_t max);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DSPCORE_H */

@@ -1,0 +1,62 @@
+"""The C-ABI library loads and exports exactly what include/dspcore.h declares;
+argument validation answers without touching a GPU."""
+import ctypes
+
+import pytest
+
+from dspcore import _lib
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = _lib.header_symbols()
+    assert len(names) == 10
+    for name in names:
+        assert hasattr(lib, name), name
+        assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_version_and_error_string():
+    lib = _lib.load()
+    assert lib.dsp_version() == 10000
+    assert isinstance(_lib.last_error(), str)
+
+
+def test_invalid_arguments_are_rejected_before_any_launch():
+    lib = _lib.load()
+    rc = lib.dsp_src_polyphase_f32(None, None, 1, 10, 10, 10, 10, None, 121, 0, 2, 0, None)
+    assert rc == _lib.DSP_EINVAL and "L=0" in _lib.last_error()
+    rc = lib.dsp_fft_r2_c2c_f32(None, None, 1, 15, 1, 1 << 15, 1 << 15, None, None)
+    assert rc == _lib.DSP_EINVAL
+    sos = (ctypes.c_double * 5)(1, 0, 0, 0, 0)
+    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 17, 1, 2048, None, 0, None)
+    assert rc == _lib.DSP_EINVAL
+    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 1, 1, 100, None, 0, None)
+    assert rc == _lib.DSP_EINVAL and "chunk_len" in _lib.last_error()
+    with pytest.raises(ValueError):
+        _lib.check(_lib.DSP_EINVAL, "x")
+    with pytest.raises(RuntimeError):
+        _lib.check(_lib.DSP_EHIP, "x")
+
+
+def test_zero_batch_is_a_no_op():
+    lib = _lib.load()
+    assert lib.dsp_src_polyphase_f32(None, None, 0, 10, 10, 15, 15, None, 121, 3, 2, 5, None) == 0
+    assert lib.dsp_spectrum_f32(None, None, 0, 10, 0, 10, 4, 9, None, None, None) == 0
+
+
+def test_workspace_query():
+    lib = _lib.load()
+    D = 12
+    B, n, T = 4096, 72000, 2048
+    C = -(-n // T)
+    need = lib.dsp_biquad_workspace_bytes(B, n, 6, T)
+    assert need >= 8 * (D * D + B * (C - 1) * D + B * C * D)
+    assert lib.dsp_biquad_workspace_bytes(B, 2000, 6, T) == 0   # single chunk: none
+    assert lib.dsp_biquad_workspace_bytes(B, n, 0, T) == 0      # clip-only: none
+
+
+def test_trace_toggle_without_gpu():
+    assert _lib.load().dsp_trace_enable(1) == 0
+    assert _lib.trace_read() == []          # nothing launched
+    assert _lib.load().dsp_trace_enable(0) == 0

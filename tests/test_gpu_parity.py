@@ -1,0 +1,302 @@
+"""Parity of the HIP path (through the C-ABI) with the reference.
+
+Expected values come from the reference's own outputs (tests/golden/*.npz) or,
+at sizes with no fixture, from the CPU oracle, which tests/test_oracle_golden.py
+pins bitwise to those fixtures.  Tolerances (measured in the
+survey container):
+  * SRC: float32 taps and accumulation -> atol 2e-6; index mapping and output
+    length bit-exact (delta inputs reproduce float32(L*h[k]) exactly);
+  * EQ: float64 coefficients and state, float32 I/O -> atol 1e-5;
+  * FFT: float32 with float64-computed twiddles -> max|dX| <= 1e-5 * max|X|;
+  * chain spectrum: the EQ tolerance propagated through the window and FFT ->
+    max|dmag| <= 1e-4 * max|mag|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_gains
+
+pytestmark = pytest.mark.gpu
+
+SRC_ATOL = 2e-6
+EQ_ATOL = 1e-5
+FFT_RTOL = 1e-5
+CHAIN_MAG_RTOL = 1e-4
+
+
+def _dc():
+    from modules import dsp_core
+    return dsp_core
+
+
+def _ops():
+    from dspcore import ops
+    return ops
+
+
+# --------------------------------------------------------------------------- SRC
+def test_src_noise_matches_reference(gpu):
+    from dspcore import design
+    g = golden("src")
+    for i, (L, M, K, N, fs) in enumerate(g["cases"]):
+        plan = design.src_plan(int(N), int(fs), int(M), int(L), None if K < 0 else int(K))
+        x = torch.from_numpy(g[f"x_{i}"]).to(gpu)
+        y = _ops().src_polyphase(x, plan).cpu().numpy()
+        ref = g[f"y_{i}"]
+        assert y.shape == ref.shape, (i, y.shape, ref.shape)
+        err = np.max(np.abs(y - ref))
+        assert err <= SRC_ATOL, f"case {i} (L={L}, M={M}, K={K}): max err {err:.3g}"
+
+
+def test_src_delta_is_bit_exact(gpu):
+    from dspcore import design
+    g = golden("src")
+    for i, (L, M, K, N) in enumerate(g["delta_cases"]):
+        plan = design.src_plan(int(N), 48000, int(M), int(L), None if K < 0 else int(K))
+        x = torch.from_numpy(g[f"dx_{i}"]).to(gpu)
+        y = _ops().src_polyphase(x, plan).cpu().numpy()
+        np.testing.assert_array_equal(y, g[f"dy_{i}"].astype(np.float32))
+
+
+def test_src_drop_in_dtypes_and_identity(gpu):
+    dc = _dc()
+    g = golden("src")
+    x = g["x_0"][0]
+    y, fs = dc.conversion_tasa_muestreo(x, 48000, 2, 3)
+    assert y.dtype == np.float64 and fs == 72000
+    assert np.max(np.abs(y - g["y_0"][0])) <= SRC_ATOL
+    same, fs1 = dc.conversion_tasa_muestreo(x, 48000, 1, 1)
+    assert same is x and fs1 == 48000
+    # keyword-only tap override (configs 2 and 5)
+    y255, _ = dc.conversion_tasa_muestreo(g["x_1"][0], 48000, 2, 3, num_taps=255)
+    assert np.max(np.abs(y255 - g["y_1"][0])) <= SRC_ATOL
+    # batched numpy and device tensors
+    yb, _ = dc.conversion_tasa_muestreo(g["x_0"], 48000, 2, 3)
+    assert yb.shape == g["y_0"].shape and np.max(np.abs(yb - g["y_0"])) <= SRC_ATOL
+    yt, _ = dc.conversion_tasa_muestreo(torch.from_numpy(x).to(gpu), 48000, 2, 3)
+    assert yt.is_cuda and yt.dtype == torch.float32
+
+
+def test_src_misaligned_rows_and_long_taps(gpu):
+    from dspcore import design
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(5)
+    # odd leading dimension (no float4 path) and the generic kernel (K = 6401)
+    for (L, M, K, N) in ((3, 2, None, 1001), (160, 147, None, 300), (7, 5, 289, 777)):
+        x = rng.uniform(-1, 1, (3, N)).astype(np.float32)
+        buf = torch.zeros((3, N + 1), dtype=torch.float32, device=gpu)
+        buf[:, :N] = torch.from_numpy(x).to(gpu)
+        plan = design.src_plan(N, 48000, M, L, K)
+        y = _ops().src_polyphase(buf[:, :N], plan).cpu().numpy()
+        for c in range(3):
+            ref, _ = orc.resample(x[c], 48000, M, L, K)
+            assert np.max(np.abs(y[c] - ref)) <= SRC_ATOL
+
+
+# --------------------------------------------------------------------------- EQ
+def test_eq_matches_reference(gpu):
+    dc = _dc()
+    g = golden("eq")
+    for i in range(10):
+        gains, fs = golden_gains(g[f"gains_{i}"]), int(g[f"fs_{i}"])
+        for src, key in (("x64", "z64"), ("x32", "z32")):
+            x = g[src]
+            z = dc.sistema_ecualizador(x, fs, gains)
+            ref = g[f"{key}_{i}"]
+            if all(abs(v) < 0.1 for v in gains.values()):
+                assert z is x, f"case {i}: bypass must return the input object"
+                continue
+            assert z.dtype == ref.dtype, (i, src, z.dtype, ref.dtype)
+            err = np.max(np.abs(z - ref))
+            assert err <= EQ_ATOL, f"case {i} {src}: max err {err:.3g}"
+
+
+def test_single_biquad_matches_lfilter(gpu):
+    import scipy.signal
+    dc = _dc()
+    x = np.random.default_rng(1).uniform(-1, 1, 5000)
+    for fc, g in ((40, 15), (10000, -15), (3000, 6)):
+        b, a = dc.disenar_coeficientes_diferencias(fc, 72000, g)
+        y = dc.aplicar_ecuacion_diferencias(x, b, a)
+        assert y.dtype == np.float64
+        assert np.max(np.abs(y - scipy.signal.lfilter(b, a, x))) <= EQ_ATOL
+
+
+def test_eq_chunk_carry_is_exact_to_rounding(gpu):
+    """Chunked carry scan vs one chunk per channel, at config-3 length."""
+    from dspcore import design
+    ops = _ops()
+    rng = np.random.default_rng(2)
+    x = torch.from_numpy(rng.uniform(-0.9, 0.9, (6, 72000)).astype(np.float32)).to(gpu)
+    sos = design.eq_plan(72000, {"Sub-Bass": 15, "Bass": -15, "Low Mids": 12,
+                                 "High Mids": -12, "Presence": 9, "Brilliance": -9}).sos
+    z_chunk = ops.biquad_cascade(x, sos, True, chunk_len=2048).cpu().numpy()
+    z_one = ops.biquad_cascade(x, sos, True, chunk_len=72000 + 32 - 72000 % 32).cpu().numpy()
+    z_small = ops.biquad_cascade(x, sos, True, chunk_len=256).cpu().numpy()
+    assert np.max(np.abs(z_chunk - z_one)) <= 1e-6
+    assert np.max(np.abs(z_small - z_one)) <= 1e-6
+
+
+def test_eq_full_length_matches_oracle(gpu):
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(3)
+    y = rng.uniform(-1, 1, (3, 72000))
+    z = _dc().sistema_ecualizador(y, 72000, orc.CONFIG3_GAINS)
+    for c in range(3):
+        ref = orc.equaliser(y[c], 72000, orc.CONFIG3_GAINS)
+        assert np.max(np.abs(z[c] - ref)) <= EQ_ATOL
+
+
+def test_eq_rows_independent_of_batch(gpu):
+    """Bitwise: a row's output does not depend on the batch it runs in."""
+    from dspcore import design
+    ops = _ops()
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy(rng.uniform(-1, 1, (9, 20000)).astype(np.float32)).to(gpu)
+    sos = design.eq_plan(72000, {"Sub-Bass": 6, "Bass": -4}).sos
+    full = ops.biquad_cascade(x, sos, True).cpu().numpy()
+    for lo, hi in ((0, 1), (1, 4), (4, 9)):
+        part = ops.biquad_cascade(x[lo:hi].contiguous(), sos, True).cpu().numpy()
+        np.testing.assert_array_equal(part, full[lo:hi])
+
+
+# --------------------------------------------------------------------------- FFT
+def test_fft_matches_reference(gpu):
+    dc = _dc()
+    g = golden("fft")
+    for k in range(13):
+        for kind in ("r", "c"):
+            x, ref = g[f"x{kind}_{k}"], g[f"X{kind}_{k}"]
+            X = dc.fft_diezmado_en_tiempo(x)
+            if k == 0:
+                assert X is x
+                continue
+            assert X.dtype == np.complex128 and X.shape == ref.shape
+            err = np.max(np.abs(X - ref))
+            assert err <= FFT_RTOL * np.max(np.abs(ref)), f"N=2^{k} {kind}: {err:.3g}"
+
+
+def test_fft_large_and_batched(gpu):
+    ops = _ops()
+    rng = np.random.default_rng(6)
+    for lg in (13, 14):
+        x = rng.uniform(-1, 1, (3, 1 << lg)) + 1j * rng.uniform(-1, 1, (3, 1 << lg))
+        X = ops.fft(torch.from_numpy(x.astype(np.complex64)).to(gpu)).cpu().numpy()
+        ref = np.fft.fft(x, axis=1)
+        assert np.max(np.abs(X - ref)) <= FFT_RTOL * np.max(np.abs(ref))
+
+
+def test_fft_rejects_non_power_of_two(gpu):
+    with pytest.raises(ValueError):
+        _dc().fft_diezmado_en_tiempo(np.ones(12))
+    with pytest.raises(ValueError):
+        _dc().fft_diezmado_en_tiempo(np.ones(3))
+
+
+# --------------------------------------------------------------------------- spectrum
+def test_spectrum_matches_reference(gpu):
+    dc = _dc()
+    g = golden("spectrum")
+    for i, n in enumerate(g["lengths"]):
+        f, m = dc.calcular_espectro_magnitud(g[f"x_{i}"], 44100)
+        np.testing.assert_array_equal(f, g[f"f_{i}"])
+        ref = g[f"m_{i}"]
+        assert m.dtype == np.float64 and m.shape == ref.shape
+        if n == 1:
+            assert np.isnan(m).all() and np.isnan(ref).all()
+            continue
+        err = np.max(np.abs(m - ref))
+        assert err <= FFT_RTOL * np.max(ref), f"len {n}: {err:.3g}"
+    for n, raised in g["raising"]:
+        if raised:
+            with pytest.raises(ValueError):
+                dc.calcular_espectro_magnitud(np.ones(int(n)), 44100)
+
+
+# --------------------------------------------------------------------------- chain
+@pytest.mark.parametrize("tag,fs,L,M,K", [("c3", 48000, 3, 2, None),
+                                          ("c5", 44100, 160, 147, 1023)])
+def test_chain_matches_reference(gpu, tag, fs, L, M, K):
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    g = golden("chain")
+    cfg = ChainConfig(48000, fs, L, M, K, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, 1, gpu)
+    x = torch.from_numpy(g[f"{tag}_x"][None, :]).to(gpu)
+    y, z, mag = (t.cpu().numpy()[0] for t in ch.run(x))
+    assert ch.fs_out == int(g[f"{tag}_fs_out"])
+    assert np.max(np.abs(y - g[f"{tag}_y"])) <= SRC_ATOL
+    assert np.max(np.abs(z - g[f"{tag}_z"])) <= EQ_ATOL
+    ref = g[f"{tag}_mag"]
+    assert np.max(np.abs(mag - ref)) <= CHAIN_MAG_RTOL * np.max(ref)
+    # the staged path (one ABI call per stage) gives the same bits
+    y2, z2, m2 = (t.cpu().numpy()[0] for t in ch.run_stages(x))
+    np.testing.assert_array_equal(y2, y)
+    np.testing.assert_array_equal(z2, z)
+    np.testing.assert_array_equal(m2, mag)
+
+
+def test_chain_config3_full_batch(gpu):
+    """Config 3 at full size (4096 x 48000): spot channels vs the oracle, and
+    every row bitwise equal to its single-row computation for a few rows."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B = 4096
+    cfg = ChainConfig(48000, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, B, gpu)
+    gen = torch.Generator(device=gpu).manual_seed(0)
+    x = torch.rand((B, 48000), generator=gen, device=gpu) * 2 - 1
+    y, z, mag = ch.run(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(z).all() and torch.isfinite(mag).all()
+    assert float(z.abs().max()) <= 1.0
+    one = Chain(cfg, 1, gpu)
+    for b in (0, 1234, B - 1):
+        xb = x[b].cpu().numpy()
+        ry, rz, _, rmag, _ = orc.chain(xb.astype(np.float32), 48000, 3, 2, orc.CONFIG3_GAINS,
+                                       None, 4096)
+        assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL
+        assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+        y1, z1, m1 = one.run(x[b:b + 1].contiguous())
+        assert torch.equal(y1[0], y[b]) and torch.equal(z1[0], z[b]) and torch.equal(m1[0], mag[b])
+
+
+def test_app_call_sequence_drop_in(gpu):
+    """app.py:164-167 then :203-205 through the drop-in module."""
+    dc = _dc()
+    g = golden("chain")
+    x = g["c3_x"]
+    gains = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3,
+             "Presence": 5, "Brilliance": -6}
+    y, fs_out = dc.conversion_tasa_muestreo(x, 48000, 2, 3)
+    z = dc.sistema_ecualizador(y, fs_out, gains)
+    assert fs_out == 72000
+    assert np.max(np.abs(z - g["c3_z"])) <= EQ_ATOL
+    f, m = dc.calcular_espectro_magnitud(z[:100000], fs_out)
+    ref = g["c3_mag2048"]
+    assert f.shape == ref.shape
+    assert np.max(np.abs(m - ref)) <= CHAIN_MAG_RTOL * np.max(ref)
+
+
+def test_shard_driver_bitwise_invariant(gpu):
+    """Sharding the batch over 1, 2, 4 or 8 'devices' (here repeated cuda:0,
+    one host thread each) gives bitwise the same result."""
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.shard import run_sharded
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1, 1, (16, 48000)).astype(np.float32)
+    cfg = ChainConfig(48000, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=4096)
+
+    def fn(xd):
+        ch = Chain(cfg, xd.shape[0], xd.device)
+        y, z, mag = ch.run(xd)
+        return z.clone(), mag.clone()
+
+    base = run_sharded(fn, x, [gpu])
+    for parts in (2, 4, 8):
+        got = run_sharded(fn, x, [gpu] * parts)
+        for a, b in zip(got, base):
+            np.testing.assert_array_equal(a, b)

@@ -1,0 +1,90 @@
+"""Host-side logic of the product path (no GPU): filter design, band selection,
+size rules and the shard partitioning, checked against the reference's outputs."""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_gains
+from dspcore import design
+from dspcore.shard import shard_ranges
+
+
+def test_sinc_taps_match_reference_bitwise():
+    g = golden("taps")
+    for i, (wc, k) in enumerate(g["cases"]):
+        np.testing.assert_array_equal(design.sinc_lowpass(wc, int(k)), g[f"h_{i}"])
+
+
+def test_biquad_design_matches_reference_bitwise():
+    for row in golden("biquad")["rows"]:
+        b, a = design.peaking_biquad(row[0], row[1], row[2])
+        np.testing.assert_array_equal(b, row[3:6])
+        np.testing.assert_array_equal(a, row[6:9])
+
+
+def test_src_plan_sizes_match_reference_outputs():
+    g = golden("src")
+    for i, (L, M, K, N, fs) in enumerate(g["cases"]):
+        p = design.src_plan(int(N), int(fs), int(M), int(L), None if K < 0 else int(K))
+        assert p.n_out == g[f"y_{i}"].shape[1]
+        assert p.fs_out == int(g[f"fs_{i}"])
+        assert p.K % 2 == 1
+        assert p.c_offset == (min(int(N) * int(L), p.K) - 1) // 2
+
+
+def test_src_plan_default_and_override_taps():
+    assert design.src_plan(48000, 48000, 2, 3).K == 121
+    assert design.src_plan(48000, 48000, 2, 3, 255).K == 255
+    assert design.src_plan(48000, 48000, 1, 2, 126).K == 127      # even -> odd
+    p = design.src_plan(48000, 44100, 147, 160, 1023)
+    assert (p.n_out, p.fs_out) == (52245, 48000)
+    with pytest.raises(ValueError):
+        design.src_plan(0, 48000, 2, 3)
+
+
+def test_eq_plan_rules():
+    g = golden("eq")
+    # bypass / clip-only / unknown band / clamp / floor, cases 3, 4, 5, 6, 8, 9
+    assert design.eq_plan(72000, golden_gains(g["gains_3"])).bypass
+    assert design.eq_plan(72000, {}).bypass
+    p = design.eq_plan(72000, golden_gains(g["gains_4"]))
+    assert not p.bypass and p.sos.shape == (0, 5)       # g == 0.1: no stage, still clips
+    p = design.eq_plan(72000, {"Mystery": 9, "Bass": 3})
+    assert p.centres == (1000, 150)
+    p = design.eq_plan(6000, golden_gains(g["gains_6"]))
+    assert max(p.centres) == pytest.approx(0.45 * 6000)
+    p = design.eq_plan(20, {"Bass": 6})
+    assert not p.bypass and p.sos.shape[0] == 0          # clamped to 9 Hz <= 10: skipped
+    p = design.eq_plan(72000, {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3,
+                               "High Mids": -3, "Presence": 5, "Brilliance": -6})
+    assert p.sos.shape == (6, 5) and p.centres == (40, 150, 1000, 3000, 5000, 10000)
+
+
+def test_spectrum_plan_matches_reference_segments():
+    g = golden("spectrum")
+    for i, n in enumerate(g["lengths"]):
+        p = design.spectrum_plan(int(n))
+        assert p.n_fft // 2 + 1 == g[f"m_{i}"].size
+    for n, raised in g["raising"]:
+        if raised:
+            with pytest.raises(ValueError):
+                design.spectrum_plan(int(n))
+        else:
+            design.spectrum_plan(int(n))
+    assert design.spectrum_plan(72000, 4096) == design.SpectrumPlan(36000, 4096, 4096)
+    assert design.spectrum_plan(0).n_fft == 2
+
+
+def test_tf_to_sos_row_normalises_like_lfilter():
+    row = design.tf_to_sos_row([2.0, 1.0], [2.0, -1.0, 0.5])
+    np.testing.assert_allclose(row, [1.0, 0.5, 0.0, -0.5, 0.25])
+    with pytest.raises(ValueError):
+        design.tf_to_sos_row([1, 2, 3, 4], [1])
+
+
+def test_shard_ranges_cover_batch_contiguously():
+    for B in (0, 1, 7, 4096, 32768):
+        for parts in (1, 2, 4, 8):
+            r = shard_ranges(B, parts)
+            assert sum(hi - lo for lo, hi in r) == B
+            assert all(r[i][1] == r[i + 1][0] for i in range(len(r) - 1))
+            assert len(r) <= parts

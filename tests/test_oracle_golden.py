@@ -1,0 +1,97 @@
+"""Pins the CPU oracle (oracle/dsp_ref_cpu.py) to the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by tests/golden/make_golden.py from
+the reference modules/dsp_core.py.  The oracle issues the same numpy/scipy calls,
+so agreement is exact (bitwise), except where the fixture itself was composed
+from reference primitives -- still exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_gains
+from oracle import dsp_ref_cpu as orc
+
+
+def test_taps_exact():
+    g = golden("taps")
+    for i, (wc, k) in enumerate(g["cases"]):
+        np.testing.assert_array_equal(orc.sinc_taps(wc, int(k)), g[f"h_{i}"])
+
+
+def test_src_noise_exact():
+    g = golden("src")
+    for i, (L, M, K, N, fs) in enumerate(g["cases"]):
+        x = g[f"x_{i}"]
+        for c in range(x.shape[0]):
+            y, fs_out = orc.resample(x[c], int(fs), int(M), int(L), None if K < 0 else int(K))
+            np.testing.assert_array_equal(y, g[f"y_{i}"][c])
+            assert fs_out == int(g[f"fs_{i}"])
+
+
+def test_src_delta_exact():
+    g = golden("src")
+    for i, (L, M, K, N) in enumerate(g["delta_cases"]):
+        x = g[f"dx_{i}"]
+        for r in range(x.shape[0]):
+            y, _ = orc.resample(x[r], 48000, int(M), int(L), None if K < 0 else int(K))
+            np.testing.assert_array_equal(y, g[f"dy_{i}"][r])
+
+
+def test_src_identity_returns_same_object():
+    x = np.arange(5, dtype=np.float32)
+    y, fs = orc.resample(x, 44100, 1, 1)
+    assert y is x and fs == 44100
+
+
+def test_biquad_exact():
+    for row in golden("biquad")["rows"]:
+        b, a = orc.peaking(row[0], row[1], row[2])
+        np.testing.assert_array_equal(b, row[3:6])
+        np.testing.assert_array_equal(a, row[6:9])
+
+
+def test_eq_exact():
+    g = golden("eq")
+    i = 0
+    while f"gains_{i}" in g:
+        gains, fs = golden_gains(g[f"gains_{i}"]), int(g[f"fs_{i}"])
+        for src, key in (("x64", "z64"), ("x32", "z32")):
+            z = orc.equaliser(g[src], fs, gains)
+            np.testing.assert_array_equal(np.asarray(z), g[f"{key}_{i}"])
+        i += 1
+    assert i == 10
+
+
+def test_fft_exact():
+    g = golden("fft")
+    for k in range(13):
+        for kind in ("r", "c"):
+            np.testing.assert_array_equal(orc.fft_dit(g[f"x{kind}_{k}"]), g[f"X{kind}_{k}"])
+
+
+def test_spectrum_exact():
+    g = golden("spectrum")
+    for i, n in enumerate(g["lengths"]):
+        with np.errstate(invalid="ignore", divide="ignore"):
+            f, m = orc.spectrum(g[f"x_{i}"], 44100)
+        np.testing.assert_array_equal(f, g[f"f_{i}"])
+        np.testing.assert_array_equal(m, g[f"m_{i}"])
+
+
+def test_spectrum_raises_where_reference_raises():
+    for n, raised in golden("spectrum")["raising"]:
+        if raised:
+            with pytest.raises(ValueError):
+                orc.spectrum(np.ones(int(n)), 44100)
+
+
+@pytest.mark.parametrize("tag,fs,L,M,K", [("c3", 48000, 3, 2, None),
+                                          ("c5", 44100, 160, 147, 1023)])
+def test_chain_exact(tag, fs, L, M, K):
+    g = golden("chain")
+    y, z, f, mag, fs_out = orc.chain(g[f"{tag}_x"], fs, L, M, orc.CONFIG3_GAINS, K, 4096)
+    assert fs_out == int(g[f"{tag}_fs_out"])
+    np.testing.assert_array_equal(y, g[f"{tag}_y"])
+    np.testing.assert_array_equal(z, g[f"{tag}_z"])
+    np.testing.assert_array_equal(mag, g[f"{tag}_mag"])
+    np.testing.assert_array_equal(orc.spectrum(z, fs_out)[1], g[f"{tag}_mag2048"])
