@@ -158,7 +158,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--channels", type=int, default=None, help="channels per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=320,
+    ap.add_argument("--cpu-sample", type=int, default=640,
                     help="channels in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=16)
     args = ap.parse_args(argv)

@@ -69,7 +69,7 @@ class Chain:
         if x.shape != (self.B, self.cfg.n_in) or x.dtype != torch.float32 or not x.is_cuda:
             raise ValueError(f"expected float32 CUDA [{self.B}, {self.cfg.n_in}], got "
                              f"{x.dtype} {tuple(x.shape)}")
-        if x.stride(1) != 1:
+        if x.stride(1) != 1 or (self.B > 1 and x.stride(0) < x.shape[1]):
             x = x.contiguous()
         return x
 
@@ -87,10 +87,10 @@ class Chain:
         with torch.cuda.device(self.device):
             rc = lib.dsp_chain_f32(
                 x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.mag.data_ptr(),
-                self.B, self.cfg.n_in, x.stride(0), self.n_out, self.y.stride(0),
+                self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.y),
                 self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
                 sos_ptr, S, clip, self.chunk_len, self.spec.seg_start, self.spec.seg_len,
-                self.spec.n_fft.bit_length() - 1, self.mag.stride(0),
+                self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(rc, "dsp_chain_f32")

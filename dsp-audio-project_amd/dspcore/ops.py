@@ -62,9 +62,14 @@ def _rows(x: torch.Tensor, name: str) -> torch.Tensor:
         raise ValueError(f"{name} must be a CUDA (ROCm) tensor")
     if x.dim() != 2:
         raise ValueError(f"{name} must be [B, n], got shape {tuple(x.shape)}")
-    if x.stride(1) != 1:
+    if x.stride(1) != 1 or (x.shape[0] > 1 and x.stride(0) < x.shape[1]):
         x = x.contiguous()
     return x
+
+
+def ld(x: torch.Tensor) -> int:
+    """Row pitch in elements (a single row's stride(0) is meaningless)."""
+    return x.stride(0) if x.shape[0] > 1 else x.shape[1]
 
 
 def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:
@@ -87,7 +92,7 @@ def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = No
     lib = _lib.load()
     with torch.cuda.device(x.device):
         rc = lib.dsp_src_polyphase_f32(
-            _ptr(x), _ptr(out), B, n_in, x.stride(0), plan.n_out, out.stride(0),
+            _ptr(x), _ptr(out), B, n_in, ld(x), plan.n_out, ld(out),
             _ptr(taps), plan.K, plan.L, plan.M, plan.c_offset, _stream(x.device))
     _lib.check(rc, "dsp_src_polyphase_f32")
     return out
@@ -116,7 +121,7 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     lib = _lib.load()
     with torch.cuda.device(x.device):
         rc = lib.dsp_biquad_cascade_f32(
-            _ptr(x), _ptr(out), B, n, x.stride(0), out.stride(0), _lib.sos_pointer(sos),
+            _ptr(x), _ptr(out), B, n, ld(x), ld(out), _lib.sos_pointer(sos),
             S, int(bool(clip)), chunk_len, _ptr(workspace), workspace.numel(),
             _stream(x.device))
     _lib.check(rc, "dsp_biquad_cascade_f32")
@@ -147,8 +152,8 @@ def fft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     tw = _table("tw", n, x.device)
     lib = _lib.load()
     with torch.cuda.device(x.device):
-        rc = lib.dsp_fft_r2_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), x.stride(0),
-                                    out.stride(0), _ptr(tw), _stream(x.device))
+        rc = lib.dsp_fft_r2_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), ld(x),
+                                    ld(out), _ptr(tw), _stream(x.device))
     _lib.check(rc, "dsp_fft_r2_c2c_f32")
     return out
 
@@ -167,7 +172,7 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
     tw = _table("tw", n_fft, x.device)
     lib = _lib.load()
     with torch.cuda.device(x.device):
-        rc = lib.dsp_spectrum_f32(_ptr(x), _ptr(out), B, x.stride(0), seg_start, seg_len,
-                                  lg, out.stride(0), _ptr(win), _ptr(tw), _stream(x.device))
+        rc = lib.dsp_spectrum_f32(_ptr(x), _ptr(out), B, ld(x), seg_start, seg_len,
+                                  lg, ld(out), _ptr(win), _ptr(tw), _stream(x.device))
     _lib.check(rc, "dsp_spectrum_f32")
     return out
