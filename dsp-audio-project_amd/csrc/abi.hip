@@ -79,11 +79,11 @@ size_t dsp_biquad_workspace_bytes(int64_t B, int64_t n, int32_t S,
 int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
                            int64_t ld_x, int64_t ld_y, const double* sos_host,
                            int32_t S, int32_t clip, int64_t chunk_len,
-                           void* workspace, size_t workspace_bytes,
-                           void* stream) {
+                           const double* state_table, void* workspace,
+                           size_t workspace_bytes, void* stream) {
   dsp::clear_error();
   return dsp::launch_biquad(x, y, B, n, ld_x, ld_y, sos_host, S, clip, chunk_len,
-                            workspace, workspace_bytes,
+                            state_table, workspace, workspace_bytes,
                             static_cast<hipStream_t>(stream));
 }
 
@@ -108,8 +108,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
                   const float* taps, int32_t K, int32_t L, int32_t M,
                   int64_t c_offset, const double* sos_host, int32_t S,
-                  int32_t clip, int64_t chunk_len, int64_t seg_start,
-                  int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  int32_t clip, int64_t chunk_len, const double* state_table,
+                  int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
                   size_t workspace_bytes, void* stream) {
   dsp::clear_error();
@@ -118,7 +118,7 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
   int rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
   if (rc) return rc;
   rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
-                          workspace, workspace_bytes, s);
+                          state_table, workspace, workspace_bytes, s);
   if (rc) return rc;
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag,
                               window, twiddles, s);

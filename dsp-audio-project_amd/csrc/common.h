@@ -71,8 +71,8 @@ int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
                int64_t n_out, int64_t ld_y, const float* taps, int K, int L,
                int M, int64_t c, hipStream_t s);
 int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
-                  int64_t ld_y, const double* sos, int S, int clip,
-                  int64_t chunk_len, void* ws, size_t ws_bytes, hipStream_t s);
+                  int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
+                  const double* state_table, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,

@@ -8,22 +8,34 @@
 // Float64 state and coefficients are mandatory: the 40 Hz band has poles at
 // |r| = 0.99926 and a float32 recursion drifts by ~1e-3.
 //
-// The recursion is serial in time, and one lane per channel leaves the chip
-// ~16x under-filled at 4096 channels.  The S-stage cascade is a 2S-state
-// linear system X' = A X + B u, so the time axis is cut into chunks of T
-// samples and the exact chunk initial states are recovered with a carry scan:
-//   pass 1 (k_iir_pass<S,false>): run every chunk but the last from zero state,
-//          keep its end state E_c                               (lanes = B*(C-1))
-//   carry  (k_iir_carry):  S_0 = 0,  S_{c+1} = A^T S_c + E_c    (lanes = B)
-//   pass 2 (k_iir_pass<S,true>):  rerun every chunk from S_c, clip, store
-// A^T is built on the device from the coefficients (k_iir_prep).  The chunk
-// length depends only on the caller's chunk_len, never on B, so a batch gives
-// bitwise-identical rows however it is sharded over GPUs.
+// Parallelism.  The recursion is serial in time and one lane per channel would
+// leave the chip ~16x under-filled at 4096 channels, and fp64 FMAs need >= 4
+// waves per SIMD to approach their issue rate (tools/ubench_fp64.hip).  The
+// S-stage cascade is a D = 2S state linear system X' = A X + B u, so each
+// channel's time axis is cut into C chunks of T samples and the exact initial
+// state of every chunk is recovered by a carry scan:
+//   pass 1: chunk end state from zero state, E_c = sum_n A^(T-1-n) B u[n]
+//           - either by running the cascade (~30 fp64 ops per sample), or
+//           - with the caller's state-response table G[t] = A^(T-1-t) B as a
+//             2S-FMA-per-sample dot product (no recurrence, no dependency chain);
+//   scan:   S_0 = 0, S_{c+1} = A^T S_c + E_c  (A^T is computed on the host);
+//   pass 2: rerun every chunk from S_c, clip, store.
+// With C <= 64 and S <= 8 all three run in ONE kernel (k_iir_fused): a block
+// holds every chunk of 4 channels, so the scan is an in-LDS sequence of
+// 2S-FMA row updates between pass 1 and pass 2.  Otherwise the general path
+// runs pass 1, a carry kernel and pass 2 as separate launches.  The chunking
+// depends only on the caller's chunk_len, never on B, so a row's result is
+// bitwise identical however the batch is sized or sharded.
 //
-// Memory: lanes are (channel, chunk) rows; a 256-row x 32-sample tile is
+// Memory.  Lanes are (channel, chunk) rows.  A 256-row x 32-sample fp32 tile is
 // loaded with coalesced 128-byte row segments into LDS (row stride 33 floats:
-// conflict-free per-lane column reads), each lane walks its row, and pass 2
-// writes its outputs back into the same tile before a coalesced store.
+// conflict-free per-lane column reads); the next tile's global loads are issued
+// into registers before the current tile is computed, so HBM latency hides
+// under the fp64 work.  Pass 2 writes its outputs back into the tile and stores
+// it with the same coalesced pattern.
+#include <cmath>
+#include <vector>
+
 #include "common.h"
 
 namespace dsp {
@@ -32,10 +44,15 @@ namespace {
 struct SosParams {
   double c[DSP_MAX_STAGES][5];  // b0 b1 b2 a1 a2
 };
+struct ScanParams {
+  double P[16 * 16];  // A^T, row-major D x D, D = 2S <= 16
+};
 
-constexpr int kIirNT = 256;
+constexpr int kNT = 256;       // lanes (rows) per block
 constexpr int kTS = 32;        // samples per tile step
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
+constexpr int kCB = 64;        // chunks per channel in the fused kernel
+constexpr int kLoads = kNT * kTS / 4 / kNT;  // float4 loads per thread per tile
 
 template <int S>
 __device__ __forceinline__ double cascade_step(double u, double (&s1)[S > 0 ? S : 1],
@@ -56,22 +73,222 @@ __device__ __forceinline__ double clip1(double v) {
   return v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
 }
 
-// APPLY = false: pass 1 (end states of chunks 0..C-2, zero initial state).
-// APPLY = true : pass 2 (all C chunks from their carried initial state).
-template <int S, bool APPLY>
-__global__ __launch_bounds__(kIirNT) void k_iir_pass(
-    const float* __restrict__ x, float* __restrict__ y, int64_t n,
-    int64_t ld_x, int64_t ld_y, SosParams p, int64_t C, int64_t T,
-    int64_t lanes, const double* __restrict__ s_init, double* __restrict__ e_out,
-    int clip, int vec_x, int vec_y) {
-  constexpr int SS = S > 0 ? S : 1;
-  __shared__ __attribute__((aligned(16))) float tile[kIirNT * kRow];
-  __shared__ int64_t row_in[kIirNT];
-  __shared__ int64_t row_out[kIirNT];
-  __shared__ int row_len[kIirNT];
+// Row descriptors live in LDS: global offset of the row's first sample for
+// input and output, and the number of valid samples in the row.
+struct Rows {
+  int64_t* in;
+  int64_t* out;
+  int* len;
+};
+
+// Issues this thread's kLoads float4 loads of tile [t0, t0+32) into registers.
+__device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restrict__ x,
+                                      const Rows& rows, int64_t t0, bool vec) {
+  const int c4 = (threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int len = rows.len[r];
+    const int64_t t = t0 + c4;
+    const float* src = x + rows.in[r] + t;
+    if (vec && t + 3 < len) {
+      v[i] = *reinterpret_cast<const float4*>(src);
+    } else {
+      v[i].x = (t + 0 < len) ? src[0] : 0.f;
+      v[i].y = (t + 1 < len) ? src[1] : 0.f;
+      v[i].z = (t + 2 < len) ? src[2] : 0.f;
+      v[i].w = (t + 3 < len) ? src[3] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads]) {
+  const int c4 = (threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    float* d = tile + (i * (kNT / 8) + (threadIdx.x >> 3)) * kRow + c4;
+    d[0] = v[i].x;
+    d[1] = v[i].y;
+    d[2] = v[i].z;
+    d[3] = v[i].w;
+  }
+}
+
+__device__ __forceinline__ void tile_store(float* __restrict__ y, const float* tile,
+                                           const Rows& rows, int64_t t0, bool vec) {
+  const int c4 = (threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int len = rows.len[r];
+    const int64_t t = t0 + c4;
+    float* dst = y + rows.out[r] + t;
+    const float* s = tile + r * kRow + c4;
+    if (vec && t + 3 < len) {
+      *reinterpret_cast<float4*>(dst) = make_float4(s[0], s[1], s[2], s[3]);
+    } else {
+      if (t + 0 < len) dst[0] = s[0];
+      if (t + 1 < len) dst[1] = s[1];
+      if (t + 2 < len) dst[2] = s[2];
+      if (t + 3 < len) dst[3] = s[3];
+    }
+  }
+}
+
+enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
+
+// One pass over every lane's row of T samples, tile by tile, with the next
+// tile's loads in flight during the current tile's arithmetic.  Samples past a
+// row's end are zeros; their outputs are never stored.  Starts with a barrier
+// (fetch reads other threads' row descriptors) and ends with one.
+template <int S, int MODE>
+__device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __restrict__ y,
+                                         float* tile, const Rows& rows, int64_t T,
+                                         double (&s1)[S > 0 ? S : 1],
+                                         double (&s2)[S > 0 ? S : 1],
+                                         double (&e)[S > 0 ? 2 * S : 1], const SosParams& p,
+                                         const double* __restrict__ G, int clip, bool vec_x,
+                                         bool vec_y) {
+  constexpr int D = 2 * S;
+  float* my = tile + threadIdx.x * kRow;
+  float4 v[kLoads];
+  __syncthreads();  // every thread's row descriptors are written
+  fetch(v, x, rows, 0, vec_x);
+  for (int64_t t0 = 0; t0 < T; t0 += kTS) {
+    __syncthreads();  // readers of the previous tile are done
+    tile_put(tile, v);
+    __syncthreads();
+    if (t0 + kTS < T) fetch(v, x, rows, t0 + kTS, vec_x);
+    if constexpr (MODE == kStateTable) {
+      const double* g = G + t0 * D;
+#pragma unroll 4
+      for (int j = 0; j < kTS; ++j) {
+        const double u = (double)my[j];
+#pragma unroll
+        for (int i = 0; i < D; ++i) e[i] = fma(g[j * D + i], u, e[i]);
+      }
+    } else {
+#pragma unroll 8
+      for (int j = 0; j < kTS; ++j) {
+        const double out = cascade_step<S>((double)my[j], s1, s2, p);
+        if constexpr (MODE == kApply) my[j] = (float)(clip ? clip1(out) : out);
+      }
+    }
+    if constexpr (MODE == kApply) {
+      __syncthreads();
+      tile_store(y, tile, rows, t0, vec_y);
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Fused single-launch cascade: pass 1 + in-LDS carry scan + pass 2.
+// Block = 4 channels x 64 chunk lanes.  C <= kCB chunks of T samples.
+// ---------------------------------------------------------------------------
+template <int S, bool GTAB>
+__global__ __launch_bounds__(kNT) void k_iir_fused(
+    const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
+    int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
+    const double* __restrict__ G, int64_t T, int C, int clip, int vec_x, int vec_y) {
+  constexpr int D = 2 * S;
+  constexpr int CHN = kNT / kCB;
+  constexpr int kTileBytes = kNT * kRow * 4;
+  constexpr int kScanBytes = kNT * D * 8;
+  __shared__ __attribute__((aligned(16)))
+  char smem[kTileBytes > kScanBytes ? kTileBytes : kScanBytes];
+  __shared__ int64_t s_in[kNT], s_out[kNT];
+  __shared__ int s_len[kNT];
+  float* tile = reinterpret_cast<float*>(smem);
+  double* scan = reinterpret_cast<double*>(smem);
 
   const int tid = threadIdx.x;
-  const int64_t g = (int64_t)blockIdx.x * kIirNT + tid;
+  const int cl = tid / kCB, c = tid % kCB;
+  const int64_t b = (int64_t)blockIdx.x * CHN + cl;
+  const bool live = b < B && c < C;
+  const int64_t t_begin = (int64_t)c * T;
+  s_in[tid] = live ? b * ld_x + t_begin : 0;
+  s_out[tid] = live ? b * ld_y + t_begin : 0;
+  s_len[tid] = live ? (int)min(T, n - t_begin) : 0;
+  const Rows rows{s_in, s_out, s_len};
+
+  double s1[S], s2[S], e[D];
+#pragma unroll
+  for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) e[i] = 0.0;
+
+  // ---- pass 1: zero-state end state of the lane's chunk
+  if constexpr (GTAB) {
+    run_pass<S, kStateTable>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+  } else {
+    run_pass<S, kStateCascade>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      e[2 * k] = s1[k];
+      e[2 * k + 1] = s2[k];
+    }
+  }
+
+  // ---- carry scan in LDS.  slot c holds E_c; step cc overwrites slot cc with
+  // S_{cc+1} = P S_cc + E_cc once E_cc has been consumed (S_cc sits in slot
+  // cc-1), so chunk c >= 1 finds its initial state in slot c-1.
+#pragma unroll
+  for (int i = 0; i < D; ++i) scan[tid * D + i] = e[i];
+  const bool row_thread = tid < CHN * D;
+  const int rc = tid / D, ri = tid - (tid / D) * D;
+  double prow[D];
+  if (row_thread) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) prow[j] = sp.P[ri * D + j];
+  }
+  __syncthreads();
+  for (int cc = 0; cc + 1 < C; ++cc) {
+    double acc = 0.0;
+    if (row_thread) {
+      const double* cur = scan + (rc * kCB + cc) * D;
+      acc = cur[ri];
+      if (cc > 0) {
+        const double* prev = cur - D;  // S_cc
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc = fma(prow[j], prev[j], acc);
+      }
+    }
+    __syncthreads();
+    if (row_thread) scan[(rc * kCB + cc) * D + ri] = acc;
+    __syncthreads();
+  }
+  if (c > 0) {
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      s1[k] = scan[(tid - 1) * D + 2 * k];
+      s2[k] = scan[(tid - 1) * D + 2 * k + 1];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
+  }
+  __syncthreads();
+
+  // ---- pass 2: outputs from the carried state
+  run_pass<S, kApply>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+}
+
+// ---------------------------------------------------------------------------
+// General path (C > kCB or S > 8): separate pass / carry launches.
+// ---------------------------------------------------------------------------
+template <int S, bool APPLY>
+__global__ __launch_bounds__(kNT) void k_iir_pass(
+    const float* __restrict__ x, float* __restrict__ y, int64_t n, int64_t ld_x,
+    int64_t ld_y, SosParams p, int64_t C, int64_t T, int64_t lanes,
+    const double* __restrict__ s_init, double* __restrict__ e_out, int clip, int vec_x,
+    int vec_y) {
+  constexpr int SS = S > 0 ? S : 1;
+  __shared__ __attribute__((aligned(16))) float tile[kNT * kRow];
+  __shared__ int64_t s_in[kNT], s_out[kNT];
+  __shared__ int s_len[kNT];
+  const int tid = threadIdx.x;
+  const int64_t g = (int64_t)blockIdx.x * kNT + tid;
   const int64_t cl = APPLY ? C : C - 1;  // chunks per channel handled here
   const bool live = g < lanes;
   int64_t b = 0, ch = 0;
@@ -80,11 +297,12 @@ __global__ __launch_bounds__(kIirNT) void k_iir_pass(
     ch = g - b * cl;
   }
   const int64_t t_begin = ch * T;
-  row_in[tid] = b * ld_x + t_begin;
-  row_out[tid] = b * ld_y + t_begin;
-  row_len[tid] = live ? (int)min(T, n - t_begin) : 0;
+  s_in[tid] = b * ld_x + t_begin;
+  s_out[tid] = b * ld_y + t_begin;
+  s_len[tid] = live ? (int)min(T, n - t_begin) : 0;
+  const Rows rows{s_in, s_out, s_len};
 
-  double s1[SS], s2[SS];
+  double s1[SS], s2[SS], e[S > 0 ? 2 * S : 1];
 #pragma unroll
   for (int k = 0; k < SS; ++k) s1[k] = s2[k] = 0.0;
   if (APPLY && live && ch > 0) {
@@ -95,76 +313,21 @@ __global__ __launch_bounds__(kIirNT) void k_iir_pass(
       s2[k] = si[2 * k + 1];
     }
   }
-  __syncthreads();
-
-  float* my = tile + tid * kRow;
-  for (int64_t t0 = 0; t0 < T; t0 += kTS) {
-    // Coalesced load: 8 threads x float4 per 128-byte row segment.
-#pragma unroll
-    for (int i = 0; i < (kIirNT * kTS / 4) / kIirNT; ++i) {
-      const int f = i * kIirNT + tid;
-      const int r = f >> 3, c4 = (f & 7) * 4;
-      const int len = row_len[r];
-      const int64_t t = t0 + c4;
-      const float* src = x + row_in[r] + t;
-      float4 v;
-      if (vec_x && t + 3 < len) {
-        v = *reinterpret_cast<const float4*>(src);
-      } else {
-        v.x = (t + 0 < len) ? src[0] : 0.f;
-        v.y = (t + 1 < len) ? src[1] : 0.f;
-        v.z = (t + 2 < len) ? src[2] : 0.f;
-        v.w = (t + 3 < len) ? src[3] : 0.f;
-      }
-      float* d = tile + r * kRow + c4;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-    __syncthreads();
-
-    // Samples past the end of a (last, partial) chunk are zeros; their
-    // outputs are never stored and that lane's final state is never used.
-#pragma unroll 8
-    for (int j = 0; j < kTS; ++j) {
-      double v = cascade_step<S>((double)my[j], s1, s2, p);
-      if (APPLY) my[j] = (float)(clip ? clip1(v) : v);
-    }
-
-    if (APPLY) {
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < (kIirNT * kTS / 4) / kIirNT; ++i) {
-        const int f = i * kIirNT + tid;
-        const int r = f >> 3, c4 = (f & 7) * 4;
-        const int len = row_len[r];
-        const int64_t t = t0 + c4;
-        float* dst = y + row_out[r] + t;
-        const float* s = tile + r * kRow + c4;
-        if (vec_y && t + 3 < len) {
-          *reinterpret_cast<float4*>(dst) = make_float4(s[0], s[1], s[2], s[3]);
-        } else {
-          if (t + 0 < len) dst[0] = s[0];
-          if (t + 1 < len) dst[1] = s[1];
-          if (t + 2 < len) dst[2] = s[2];
-          if (t + 3 < len) dst[3] = s[3];
-        }
-      }
-    }
-    __syncthreads();
-  }
-
+  run_pass<S, APPLY ? kApply : kStateCascade>(x, y, tile, rows, T, s1, s2, e, p, nullptr,
+                                              clip, vec_x != 0, vec_y != 0);
   if (!APPLY && live) {
-    double* e = e_out + g * (2 * S);
+    double* eo = e_out + g * (2 * S);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      e[2 * k] = s1[k];
-      e[2 * k + 1] = s2[k];
+      eo[2 * k] = s1[k];
+      eo[2 * k + 1] = s2[k];
     }
   }
 }
 
-// One lane per channel: S_0 = 0, S_{c+1} = P S_c + E_c, P = A^T (D x D).
-// The state vectors live in LDS ([D][256] doubles, double-buffered) so the
-// kernel stays small for every D; it is a few microseconds of serial work.
+// One lane per channel: S_0 = 0, S_{c+1} = P S_c + E_c.  The state vectors
+// live in LDS ([D][256] doubles, double-buffered) so the kernel stays small for
+// every D.
 template <int S>
 __global__ __launch_bounds__(256) void k_iir_carry(const double* __restrict__ P,
                                                    const double* __restrict__ E,
@@ -195,14 +358,14 @@ __global__ __launch_bounds__(256) void k_iir_carry(const double* __restrict__ P,
 }
 
 // Builds A (one cascade step on each unit state, zero input) and P = A^T by
-// square-and-multiply, all in float64 inside one workgroup.
+// square-and-multiply in float64 inside one workgroup (general path; the fused
+// path gets A^T from the host as a kernel argument).
 __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T,
                                                   double* __restrict__ P_out) {
   __shared__ double sA[32 * 32], sR[32 * 32], sTmp[32 * 32];
   const int D = 2 * S;
   const int tid = threadIdx.x;
   if (tid < D) {
-    // state vector e_tid: s1_k = X[2k], s2_k = X[2k+1]
     double X[32];
     for (int i = 0; i < D; ++i) X[i] = (i == tid) ? 1.0 : 0.0;
     double u = 0.0;
@@ -242,16 +405,65 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
   if (r < D && c < D) P_out[r * D + c] = sR[r * D + c];
 }
 
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+// A of the D = 2S state system (state order s1_0, s2_0, s1_1, ...), float64.
+std::vector<double> state_matrix(const SosParams& p, int S) {
+  const int D = 2 * S;
+  std::vector<double> A((size_t)D * D, 0.0);
+  for (int col = 0; col < D; ++col) {
+    std::vector<double> X(D, 0.0);
+    X[col] = 1.0;
+    double u = 0.0;
+    for (int k = 0; k < S; ++k) {
+      const double v = p.c[k][0] * u + X[2 * k];
+      const double n1 = p.c[k][1] * u - p.c[k][3] * v + X[2 * k + 1];
+      const double n2 = p.c[k][2] * u - p.c[k][4] * v;
+      X[2 * k] = n1;
+      X[2 * k + 1] = n2;
+      u = v;
+    }
+    for (int r = 0; r < D; ++r) A[(size_t)r * D + col] = X[r];
+  }
+  return A;
+}
+
+std::vector<double> matmul(const std::vector<double>& a, const std::vector<double>& b, int D) {
+  std::vector<double> c((size_t)D * D, 0.0);
+  for (int i = 0; i < D; ++i)
+    for (int k = 0; k < D; ++k) {
+      const double aik = a[(size_t)i * D + k];
+      for (int j = 0; j < D; ++j)
+        c[(size_t)i * D + j] = std::fma(aik, b[(size_t)k * D + j], c[(size_t)i * D + j]);
+    }
+  return c;
+}
+
+// A^T by square-and-multiply.
+std::vector<double> chunk_transition(const SosParams& p, int S, int64_t T) {
+  const int D = 2 * S;
+  std::vector<double> base = state_matrix(p, S), r((size_t)D * D, 0.0);
+  for (int i = 0; i < D; ++i) r[(size_t)i * D + i] = 1.0;
+  for (int64_t e = T; e > 0; e >>= 1) {
+    if (e & 1) r = matmul(r, base, D);
+    if (e > 1) base = matmul(base, base, D);
+  }
+  return r;
+}
+
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct WsLayout {
   size_t p_off, e_off, s_off, total;
 };
 
+bool fused_ok(int S, int64_t C) { return S >= 1 && S <= 8 && S != 7 && C >= 2 && C <= kCB; }
+
 WsLayout ws_layout(int64_t B, int64_t n, int S, int64_t T) {
   WsLayout w{0, 0, 0, 0};
   const int64_t C = (S == 0 || T <= 0) ? 1 : ceil_div(n, T);
-  if (C <= 1) return w;
+  if (C <= 1 || fused_ok(S, C)) return w;
   const size_t D = 2 * (size_t)S;
   w.p_off = 0;
   w.e_off = align256(D * D * sizeof(double));
@@ -260,12 +472,39 @@ WsLayout ws_layout(int64_t B, int64_t n, int S, int64_t T) {
   return w;
 }
 
+int padded_stages(int S) {
+  if (S == 7) return 8;
+  if (S > 8 && S <= 12) return 12;
+  if (S > 12) return 16;
+  return S;
+}
+
 template <int S>
-int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
-                int64_t ld_y, const SosParams& p, int clip, int64_t T, void* ws,
+int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
+              const SosParams& p, int clip, int64_t T, const double* G, int vec_x, int vec_y,
+              hipStream_t s) {
+  static_assert(2 * S <= 16, "scan matrix is at most 16 x 16");
+  ScanParams sp;
+  const std::vector<double> P = chunk_transition(p, S, T);
+  for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
+  const int C = (int)ceil_div(n, T);
+  constexpr int CHN = kNT / kCB;
+  const dim3 grid((unsigned)ceil_div(B, CHN));
+  TraceScope trace("iir_fused", s);
+  if (G)
+    hipLaunchKernelGGL((k_iir_fused<S, true>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, ld_y,
+                       p, sp, G, T, C, clip, vec_x, vec_y);
+  else
+    hipLaunchKernelGGL((k_iir_fused<S, false>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, ld_y,
+                       p, sp, G, T, C, clip, vec_x, vec_y);
+  DSP_LAUNCHED("k_iir_fused");
+  return DSP_OK;
+}
+
+template <int S>
+int run_general(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
+                const SosParams& p, int clip, int64_t T, void* ws, int vec_x, int vec_y,
                 hipStream_t s) {
-  const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
-  const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
   const int64_t C = (S == 0) ? 1 : ceil_div(n, T);
   if (C == 1) T = ceil_div(n, kTS) * kTS;
   const WsLayout w = ws_layout(B, n, S, T);
@@ -275,63 +514,71 @@ int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
   double* SI = reinterpret_cast<double*>(base + w.s_off);
   if (C > 1) {
     {
-    TraceScope trace("iir_prep", s);
-    hipLaunchKernelGGL(k_iir_prep, dim3(1), dim3(1024), 0, s, p, S, T, P);
+      TraceScope trace("iir_prep", s);
+      hipLaunchKernelGGL(k_iir_prep, dim3(1), dim3(1024), 0, s, p, S, T, P);
     }
     DSP_LAUNCHED("k_iir_prep");
     const int64_t lanes1 = B * (C - 1);
     {
-    TraceScope trace("iir_state", s);
-    hipLaunchKernelGGL((k_iir_pass<S, false>), dim3((unsigned)ceil_div(lanes1, kIirNT)),
-                       dim3(kIirNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes1,
-                       (const double*)nullptr, E, clip, vec_x, vec_y);
+      TraceScope trace("iir_state", s);
+      hipLaunchKernelGGL((k_iir_pass<S, false>), dim3((unsigned)ceil_div(lanes1, kNT)),
+                         dim3(kNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes1,
+                         (const double*)nullptr, E, clip, vec_x, vec_y);
     }
     DSP_LAUNCHED("k_iir_pass<state>");
     {
-    TraceScope trace("iir_carry", s);
-    hipLaunchKernelGGL((k_iir_carry<(S > 0 ? S : 1)>), dim3((unsigned)ceil_div(B, 256)),
-                       dim3(256), 0, s, P, E, SI, B, C);
+      TraceScope trace("iir_carry", s);
+      hipLaunchKernelGGL((k_iir_carry<(S > 0 ? S : 1)>), dim3((unsigned)ceil_div(B, 256)),
+                         dim3(256), 0, s, P, E, SI, B, C);
     }
     DSP_LAUNCHED("k_iir_carry");
   }
   const int64_t lanes2 = B * C;
   {
-  TraceScope trace("iir_apply", s);
-  hipLaunchKernelGGL((k_iir_pass<S, true>), dim3((unsigned)ceil_div(lanes2, kIirNT)),
-                     dim3(kIirNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes2,
-                     SI, (double*)nullptr, clip, vec_x, vec_y);
+    TraceScope trace("iir_apply", s);
+    hipLaunchKernelGGL((k_iir_pass<S, true>), dim3((unsigned)ceil_div(lanes2, kNT)),
+                       dim3(kNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes2, SI,
+                       (double*)nullptr, clip, vec_x, vec_y);
   }
   DSP_LAUNCHED("k_iir_pass<apply>");
   return DSP_OK;
+}
+
+template <int S>
+int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
+                const SosParams& p, int clip, int64_t T, const double* G, void* ws,
+                hipStream_t s) {
+  const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
+  const int64_t C = (S == 0) ? 1 : ceil_div(n, T);
+  if constexpr (S >= 1 && S <= 8 && S != 7) {
+    if (fused_ok(S, C))
+      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, vec_x, vec_y, s);
+  }
+  return run_general<S>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
 }
 
 }  // namespace
 
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len) {
   if (B <= 0 || n <= 0 || S < 0 || S > DSP_MAX_STAGES || chunk_len <= 0) return 0;
-  int Sp = S;
-  if (S == 7) Sp = 8;
-  else if (S > 8 && S <= 12) Sp = 12;
-  else if (S > 12) Sp = 16;
-  return ws_layout(B, n, Sp, chunk_len).total;
+  return ws_layout(B, n, padded_stages(S), chunk_len).total;
 }
 
 int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
-                  int64_t ld_y, const double* sos, int S, int clip,
-                  int64_t chunk_len, void* ws, size_t ws_bytes, hipStream_t s) {
+                  int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
+                  const double* state_table, void* ws, size_t ws_bytes, hipStream_t s) {
   DSP_REQUIRE(B >= 0 && n >= 0, "bad sizes");
   DSP_REQUIRE(S >= 0 && S <= DSP_MAX_STAGES, "S=%d outside [0, %d]", S, DSP_MAX_STAGES);
   DSP_REQUIRE(chunk_len > 0 && chunk_len % kTS == 0,
               "chunk_len=%lld must be a positive multiple of %d", (long long)chunk_len, kTS);
+  DSP_REQUIRE(chunk_len <= (int64_t)1 << 30, "chunk_len too large");
   DSP_REQUIRE(ld_x >= n && ld_y >= n, "leading dimension too small");
   if (B == 0 || n == 0) return DSP_OK;
   DSP_REQUIRE(x && y, "null pointer");
   DSP_REQUIRE(S == 0 || sos, "null sos");
   // Pad S up to an instantiated size with exact identity stages (b = 1,0,0; a = 0,0).
-  int Sp = S;
-  if (S == 7) Sp = 8;
-  else if (S > 8 && S <= 12) Sp = 12;
-  else if (S > 12) Sp = 16;
+  const int Sp = padded_stages(S);
   SosParams p;
   for (int k = 0; k < DSP_MAX_STAGES; ++k) {
     for (int i = 0; i < 5; ++i) p.c[k][i] = (k < S) ? sos[5 * k + i] : (i == 0 ? 1.0 : 0.0);
@@ -339,17 +586,19 @@ int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
   const size_t need = ws_layout(B, n, Sp, chunk_len).total;
   DSP_REQUIRE(ws_bytes >= need, "workspace too small: %zu < %zu bytes", ws_bytes, need);
   DSP_REQUIRE(need == 0 || ws, "null workspace");
+  // The state-response table is laid out for exactly S stages.
+  const double* G = (Sp == S) ? state_table : nullptr;
   switch (Sp) {
-    case 0: return run_cascade<0>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 1: return run_cascade<1>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 2: return run_cascade<2>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 3: return run_cascade<3>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 4: return run_cascade<4>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 5: return run_cascade<5>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 6: return run_cascade<6>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 8: return run_cascade<8>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 12: return run_cascade<12>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
-    case 16: return run_cascade<16>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, ws, s);
+    case 0: return run_cascade<0>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 1: return run_cascade<1>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 2: return run_cascade<2>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 3: return run_cascade<3>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 4: return run_cascade<4>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 5: return run_cascade<5>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 6: return run_cascade<6>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 8: return run_cascade<8>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 12: return run_cascade<12>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 16: return run_cascade<16>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
 }

@@ -210,14 +210,16 @@ int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
 
   // Register-blocked instantiations: the benchmark configurations and the
   // app's most common (L, M) pairs with the default tap rule 40*max(L,M)+1.
+  // R is chosen so that R*M is not a multiple of 32: thread groups' windows
+  // start R*M floats apart and must land on different LDS banks.
   if (L == 3 && M == 2 && T == 41)
-    return run_reg<3, 2, 41, 16, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+    return run_reg<3, 2, 41, 15, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
   if (L == 3 && M == 2 && T == 85)
-    return run_reg<3, 2, 85, 8, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+    return run_reg<3, 2, 85, 7, 192>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
   if (L == 2 && M == 1 && T == 64)
-    return run_reg<2, 1, 64, 16, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+    return run_reg<2, 1, 64, 15, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
   if (L == 2 && M == 1 && T == 41)
-    return run_reg<2, 1, 41, 16, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
+    return run_reg<2, 1, 41, 15, 256>(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, c, vec_x, vec_y, s);
 
   // Generic path.  Shrink the tile until bank + window fit in LDS.
   const int bank_floats = ((L * T + 3) / 4) * 4;

@@ -42,7 +42,7 @@ _SIGNATURES = {
     "dsp_biquad_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i64]),
     "dsp_biquad_cascade_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _dp, _c_i32, _c_i32, _c_i64,
-        _vp, _c_sz, _vp]),
+        _vp, _vp, _c_sz, _vp]),
     "dsp_fft_r2_c2c_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp]),
     "dsp_spectrum_f32": (ctypes.c_int, [
@@ -50,7 +50,7 @@ _SIGNATURES = {
         _vp]),
     "dsp_chain_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
-        _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _c_i64,
+        _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _c_i64,
         _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "dsp_trace_enable": (ctypes.c_int, [_c_i32]),
     "dsp_trace_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _c_i32]),

@@ -12,7 +12,8 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from .design import EqPlan, SpectrumPlan, SrcPlan, eq_plan, spectrum_plan, src_plan
+from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, spectrum_plan,
+                     src_plan)
 
 
 @dataclass(frozen=True)
@@ -31,7 +32,7 @@ class Chain:
     """Device-resident plan of the chain for a fixed batch size."""
 
     def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
-                 chunk_len: int = ops.CHUNK_LEN):
+                 chunk_len: int | None = None, use_table: bool = True):
         ops.require_gpu()
         self.cfg = cfg
         self.B = int(batch)
@@ -46,7 +47,7 @@ class Chain:
         self.eq: EqPlan = eq_plan(self.fs_out, cfg.gains)
         spec_len = n_out if cfg.limit_pts is None else min(n_out, cfg.limit_pts)
         self.spec: SpectrumPlan = spectrum_plan(spec_len, cfg.n_fft)
-        self.chunk_len = int(chunk_len)
+        self.chunk_len = chunk_len_for(n_out) if chunk_len is None else int(chunk_len)
         dev = self.device
         self.taps = ops.taps_tensor(self.src, dev)
         self.window = ops._table("hann", self.spec.n_fft, dev)
@@ -58,6 +59,7 @@ class Chain:
                                device=dev)
         self.workspace = ops.biquad_workspace(self.B, n_out, self.sos.shape[0], dev,
                                               self.chunk_len)
+        self.table = ops.state_table(self.sos, self.chunk_len, dev) if use_table else None
 
     # -- algorithmic traffic ---------------------------------
     def algorithmic_bytes(self) -> int:
@@ -89,7 +91,8 @@ class Chain:
                 x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.mag.data_ptr(),
                 self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.y),
                 self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
-                sos_ptr, S, clip, self.chunk_len, self.spec.seg_start, self.spec.seg_len,
+                sos_ptr, S, clip, self.chunk_len, ops._ptr(self.table), self.spec.seg_start,
+                self.spec.seg_len,
                 self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)
@@ -116,7 +119,7 @@ class Chain:
             z = y                       # dsp_core.py:222-223 returns its input
         else:
             z = ops.biquad_cascade(y, self.sos, True, out=self.z, workspace=self.workspace,
-                                   chunk_len=self.chunk_len)
+                                   chunk_len=self.chunk_len, use_table=self.table is not None)
         mark(1, 1)
         mark(2, 0)
         ops.spectrum(z, self.spec.seg_start, self.spec.seg_len, self.spec.n_fft, out=self.mag)

@@ -155,6 +155,53 @@ def tf_to_sos_row(b, a) -> np.ndarray:
     return np.array([bb[0], bb[1], bb[2], aa[1], aa[2]])
 
 
+def chunk_len_for(n: int, max_chunks: int = 64) -> int:
+    """Chunk length of the biquad carry scan for a row of n samples: the
+    smallest multiple of 32 that splits the row into <= max_chunks chunks, so the
+    cascade runs as one fused launch (include/dspcore.h).  A function of n
+    only: every row's result is independent of the batch size."""
+    per = -(-int(n) // max_chunks)
+    return max(32, -(-per // 32) * 32)
+
+
+def state_space(sos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """(A, B) of the S-stage DF2T cascade as one D = 2S state system
+    X' = A X + B u, state order (s1_0, s2_0, s1_1, s2_1, ...)."""
+    sos = np.asarray(sos, dtype=np.float64).reshape(-1, 5)
+    S = sos.shape[0]
+    D = 2 * S
+
+    def step(X, u):
+        X = X.copy()
+        for k in range(S):
+            b0, b1, b2, a1, a2 = sos[k]
+            v = b0 * u + X[2 * k]
+            X[2 * k], X[2 * k + 1] = b1 * u - a1 * v + X[2 * k + 1], b2 * u - a2 * v
+            u = v
+        return X
+
+    A = np.column_stack([step(np.eye(D)[i], 0.0) for i in range(D)]) if D else np.zeros((0, 0))
+    B = step(np.zeros(D), 1.0)
+    return A, B
+
+
+def state_response_table(sos: np.ndarray, chunk_len: int) -> np.ndarray:
+    """float64 [chunk_len][2S]: row t = A^(chunk_len-1-t) B, the cascade state at
+    the end of a chunk caused by a unit sample t samples into it.  The GPU
+    cascade turns its chunk end states into one dot product per state with it."""
+    A, B = state_space(sos)
+    D = B.size
+    G = np.empty((chunk_len, D))
+    G[0] = B
+    m, Am = 1, A.copy()
+    while m < chunk_len:
+        k = min(m, chunk_len - m)
+        G[m:m + k] = G[:k] @ Am.T          # A^m applied to rows 0..k-1
+        m += k
+        Am = Am @ Am
+    return np.ascontiguousarray(G[::-1])
+
+
 @dataclass(frozen=True)
 class SpectrumPlan:
     seg_start: int

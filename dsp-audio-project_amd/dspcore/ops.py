@@ -14,11 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .design import SrcPlan, hann, twiddles
-
-# Chunk length of the biquad carry scan.  Fixed (not derived from the batch)
-# so every row's result is bitwise independent of batch size and sharding.
-CHUNK_LEN = 2048
+from .design import SrcPlan, chunk_len_for, hann, state_response_table, twiddles
 
 _tables_lock = threading.Lock()
 _tables: dict = {}
@@ -99,14 +95,35 @@ def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = No
 
 
 def biquad_workspace(B: int, n: int, S: int, device: torch.device,
-                     chunk_len: int = CHUNK_LEN) -> torch.Tensor:
+                     chunk_len: int | None = None) -> torch.Tensor:
+    chunk_len = chunk_len_for(n) if chunk_len is None else chunk_len
     nbytes = _lib.load().dsp_biquad_workspace_bytes(B, n, S, chunk_len)
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
+def state_table(sos: np.ndarray, chunk_len: int, device: torch.device) -> torch.Tensor | None:
+    """Cached device copy of design.state_response_table (None when the fused
+    kernel cannot use it: S == 0, S == 7 or S > 8)."""
+    S = sos.shape[0]
+    if S == 0 or S == 7 or S > 8:
+        return None
+    key = ("G", sos.tobytes(), chunk_len, device.index)
+    t = _tables.get(key)
+    if t is None:
+        with _tables_lock:
+            t = _tables.get(key)
+            if t is None:
+                if len(_tables) > 256:  # bound the cache under slider sweeps
+                    for k in [k for k in _tables if k[0] == "G"]:
+                        del _tables[k]
+                t = torch.from_numpy(state_response_table(sos, chunk_len)).to(device)
+                _tables[key] = t
+    return t
+
+
 def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
                    out: torch.Tensor | None = None, workspace: torch.Tensor | None = None,
-                   chunk_len: int = CHUNK_LEN) -> torch.Tensor:
+                   chunk_len: int | None = None, use_table: bool = True) -> torch.Tensor:
     """z = clip(cascade(x)) per row (dsp_core.py:233-254), fp64 inside, fp32 I/O."""
     x = _rows(x, "x")
     if x.dtype != torch.float32:
@@ -114,15 +131,17 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     sos = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 5)
     B, n = x.shape
     S = sos.shape[0]
+    chunk_len = chunk_len_for(n) if chunk_len is None else int(chunk_len)
     if out is None:
         out = torch.empty_like(x)
     if workspace is None:
         workspace = biquad_workspace(B, n, S, x.device, chunk_len)
+    table = state_table(sos, chunk_len, x.device) if use_table else None
     lib = _lib.load()
     with torch.cuda.device(x.device):
         rc = lib.dsp_biquad_cascade_f32(
             _ptr(x), _ptr(out), B, n, ld(x), ld(out), _lib.sos_pointer(sos),
-            S, int(bool(clip)), chunk_len, _ptr(workspace), workspace.numel(),
+            S, int(bool(clip)), chunk_len, _ptr(table), _ptr(workspace), workspace.numel(),
             _stream(x.device))
     _lib.check(rc, "dsp_biquad_cascade_f32")
     return out

@@ -69,16 +69,22 @@ int dsp_src_polyphase_f32(const float* x, float* y, int64_t B, int64_t n_in,
  * `sos_host` is a HOST array [S][5] = {b0, b1, b2, a1, a2} per stage, a0 == 1,
  * float64; coefficients and state are float64 inside the kernel, I/O float32.
  * The time axis is cut into chunks of `chunk_len` samples (multiple of 32)
- * whose initial states are recovered by a linear-recurrence carry pass, so
+ * whose initial states are recovered by a linear-recurrence carry scan, so
  * results do not depend on B or on how a batch is sharded.  x may equal y.
+ * With S <= 8 (S != 7) and ceil(n / chunk_len) <= 64 the whole cascade is one
+ * launch and needs no workspace.  `state_table` (optional, device, may be
+ * NULL) is float64 [chunk_len][2S]: row t = A^(chunk_len-1-t) B, the state
+ * response of the S-stage cascade (state order s1_0, s2_0, s1_1, ...) to a
+ * unit sample t samples into a chunk; with it the chunk end states cost 2S
+ * FMAs per sample instead of a cascade run.
  * ------------------------------------------------------------------------- */
 size_t dsp_biquad_workspace_bytes(int64_t B, int64_t n, int32_t S,
                                   int64_t chunk_len);
 int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
                            int64_t ld_x, int64_t ld_y, const double* sos_host,
                            int32_t S, int32_t clip, int64_t chunk_len,
-                           void* workspace, size_t workspace_bytes,
-                           void* stream);
+                           const double* state_table, void* workspace,
+                           size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Radix-2 decimation-in-time FFT, batched, natural-order output.
@@ -116,8 +122,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
                   const float* taps, int32_t K, int32_t L, int32_t M,
                   int64_t c_offset, const double* sos_host, int32_t S,
-                  int32_t clip, int64_t chunk_len, int64_t seg_start,
-                  int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  int32_t clip, int64_t chunk_len, const double* state_table,
+                  int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
                   size_t workspace_bytes, void* stream);
 

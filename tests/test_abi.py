@@ -29,9 +29,9 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     rc = lib.dsp_fft_r2_c2c_f32(None, None, 1, 15, 1, 1 << 15, 1 << 15, None, None)
     assert rc == _lib.DSP_EINVAL
     sos = (ctypes.c_double * 5)(1, 0, 0, 0, 0)
-    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 17, 1, 2048, None, 0, None)
+    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 17, 1, 2048, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL
-    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 1, 1, 100, None, 0, None)
+    rc = lib.dsp_biquad_cascade_f32(None, None, 1, 100, 100, 100, sos, 1, 1, 100, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL and "chunk_len" in _lib.last_error()
     with pytest.raises(ValueError):
         _lib.check(_lib.DSP_EINVAL, "x")
@@ -50,8 +50,12 @@ def test_workspace_query():
     D = 12
     B, n, T = 4096, 72000, 2048
     C = -(-n // T)
-    need = lib.dsp_biquad_workspace_bytes(B, n, 6, T)
+    assert lib.dsp_biquad_workspace_bytes(B, n, 6, 1152) == 0       # fused: none
+    need = lib.dsp_biquad_workspace_bytes(B, n, 6, 256)             # 282 chunks
+    C = -(-n // 256)
     assert need >= 8 * (D * D + B * (C - 1) * D + B * C * D)
+    need9 = lib.dsp_biquad_workspace_bytes(B, n, 9, T)              # S > 8: general
+    assert need9 > 0
     assert lib.dsp_biquad_workspace_bytes(B, 2000, 6, T) == 0   # single chunk: none
     assert lib.dsp_biquad_workspace_bytes(B, n, 0, T) == 0      # clip-only: none
 

@@ -124,18 +124,38 @@ def test_single_biquad_matches_lfilter(gpu):
 
 
 def test_eq_chunk_carry_is_exact_to_rounding(gpu):
-    """Chunked carry scan vs one chunk per channel, at config-3 length."""
+    """Every scan variant vs one chunk per channel (a plain serial recursion),
+    at config-3 length: fused kernel with / without the state-response table,
+    and the general three-launch path (282 chunks)."""
     from dspcore import design
     ops = _ops()
     rng = np.random.default_rng(2)
     x = torch.from_numpy(rng.uniform(-0.9, 0.9, (6, 72000)).astype(np.float32)).to(gpu)
     sos = design.eq_plan(72000, {"Sub-Bass": 15, "Bass": -15, "Low Mids": 12,
                                  "High Mids": -12, "Presence": 9, "Brilliance": -9}).sos
-    z_chunk = ops.biquad_cascade(x, sos, True, chunk_len=2048).cpu().numpy()
     z_one = ops.biquad_cascade(x, sos, True, chunk_len=72000 + 32 - 72000 % 32).cpu().numpy()
-    z_small = ops.biquad_cascade(x, sos, True, chunk_len=256).cpu().numpy()
-    assert np.max(np.abs(z_chunk - z_one)) <= 1e-6
-    assert np.max(np.abs(z_small - z_one)) <= 1e-6
+    variants = {
+        "fused+table": dict(),
+        "fused": dict(use_table=False),
+        "fused, 36 chunks": dict(chunk_len=2048),
+        "general, 282 chunks": dict(chunk_len=256),
+    }
+    for name, kw in variants.items():
+        z = ops.biquad_cascade(x, sos, True, **kw).cpu().numpy()
+        assert np.max(np.abs(z - z_one)) <= 1e-6, name
+
+
+def test_eq_many_stages_general_path(gpu):
+    """S = 9 (padded to 12: general three-launch path) and S = 7 (padded to 8:
+    fused kernel without the state table)."""
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(8)
+    y = rng.uniform(-1, 1, (2, 30000))
+    for gains in ({f"b{i}": (-1) ** i * (3 + i) for i in range(9)},
+                  {**{k: 4 for k in orc.CONFIG3_GAINS}, "extra": -5}):
+        z = _dc().sistema_ecualizador(y, 72000, gains)
+        for c in range(2):
+            assert np.max(np.abs(z[c] - orc.equaliser(y[c], 72000, gains))) <= EQ_ATOL
 
 
 def test_eq_full_length_matches_oracle(gpu):

@@ -88,3 +88,35 @@ def test_shard_ranges_cover_batch_contiguously():
             assert sum(hi - lo for lo, hi in r) == B
             assert all(r[i][1] == r[i + 1][0] for i in range(len(r) - 1))
             assert len(r) <= parts
+
+
+def _cascade_end_state(sos, u):
+    """Reference DF2T recursion (lfilter's form) returning the final stage states."""
+    S = sos.shape[0]
+    st = np.zeros(2 * S)
+    for x in u:
+        v = x
+        for k in range(S):
+            b0, b1, b2, a1, a2 = sos[k]
+            out = b0 * v + st[2 * k]
+            st[2 * k], st[2 * k + 1] = b1 * v - a1 * out + st[2 * k + 1], b2 * v - a2 * out
+            v = out
+    return st
+
+
+def test_state_response_table_gives_chunk_end_states():
+    sos = design.eq_plan(72000, {"Sub-Bass": 15, "Bass": -9, "Presence": 6}).sos
+    rng = np.random.default_rng(0)
+    for T in (32, 96, 1152):
+        u = rng.uniform(-1, 1, T)
+        G = design.state_response_table(sos, T)
+        assert G.shape == (T, 2 * sos.shape[0])
+        np.testing.assert_allclose(u @ G, _cascade_end_state(sos, u), rtol=0, atol=1e-11)
+
+
+def test_chunk_policy_is_batch_independent_and_fused():
+    for n in (1, 31, 32, 100, 4800, 72000, 52245, 10 ** 6):
+        T = design.chunk_len_for(n)
+        assert T % 32 == 0 and T >= 32
+        assert -(-n // T) <= 64
+    assert design.chunk_len_for(72000) == 1152
