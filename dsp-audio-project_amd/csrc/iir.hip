@@ -51,7 +51,7 @@ struct ScanParams {
 constexpr int kNT = 256;       // lanes (rows) per block
 constexpr int kTS = 32;        // samples per tile step
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
-constexpr int kCB = 64;        // chunks per channel in the fused kernel
+constexpr int kCBMax = 256;    // max chunks per channel in the fused kernel
 constexpr int kLoads = kNT * kTS / 4 / kNT;  // float4 loads per thread per tile
 
 template <int S>
@@ -82,18 +82,25 @@ struct Rows {
 };
 
 // Issues this thread's kLoads float4 loads of tile [t0, t0+32) into registers.
+// VEC (rows 16-byte aligned, ld % 4 == 0): branch-free -- every vector with at
+// least one valid sample is loaded whole (ld % 4 == 0 and ld >= n keep the
+// over-read inside the row pitch), others load a dummy vector at x; masking is
+// deferred to tile_put so no wait lands between the loads and their use.
+// !VEC: guarded scalar loads (slow path for odd pitches).
+template <bool VEC>
 __device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restrict__ x,
-                                      const Rows& rows, int64_t t0, bool vec) {
+                                      const Rows& rows, int64_t t0) {
   const int c4 = (threadIdx.x & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
     const int r = i * (kNT / 8) + (threadIdx.x >> 3);
     const int len = rows.len[r];
     const int64_t t = t0 + c4;
-    const float* src = x + rows.in[r] + t;
-    if (vec && t + 3 < len) {
+    if constexpr (VEC) {
+      const float* src = (t < len) ? x + rows.in[r] + t : x;
       v[i] = *reinterpret_cast<const float4*>(src);
     } else {
+      const float* src = x + rows.in[r] + t;
       v[i].x = (t + 0 < len) ? src[0] : 0.f;
       v[i].y = (t + 1 < len) ? src[1] : 0.f;
       v[i].z = (t + 2 < len) ? src[2] : 0.f;
@@ -102,37 +109,78 @@ __device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restri
   }
 }
 
-__device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads]) {
+// Writes the fetched tile into LDS, zeroing samples past each row's end.
+__device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads],
+                                         const Rows& rows, int64_t t0) {
   const int c4 = (threadIdx.x & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
-    float* d = tile + (i * (kNT / 8) + (threadIdx.x >> 3)) * kRow + c4;
-    d[0] = v[i].x;
-    d[1] = v[i].y;
-    d[2] = v[i].z;
-    d[3] = v[i].w;
+    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int64_t t = t0 + c4;
+    const int len = rows.len[r];
+    float* d = tile + r * kRow + c4;
+    d[0] = (t + 0 < len) ? v[i].x : 0.f;
+    d[1] = (t + 1 < len) ? v[i].y : 0.f;
+    d[2] = (t + 2 < len) ? v[i].z : 0.f;
+    d[3] = (t + 3 < len) ? v[i].w : 0.f;
   }
 }
 
-__device__ __forceinline__ void tile_store(float* __restrict__ y, const float* tile,
-                                           const Rows& rows, int64_t t0, bool vec) {
+// Stores this thread's kLoads vectors of the tile.  SM (store mode):
+//   0: guarded float4 / scalar global stores (any pitch; general path);
+//   1: one raw-buffer float4 store per vector, offset pushed out of range when
+//      the vector is past the row's end -- branch-free, so the compiler can
+//      count vmcnt exactly and the next tile's wait never drains these stores;
+//   2: like 1 with four dword stores per vector (rows whose length is not a
+//      multiple of 4 end in a partial vector).
+// Modes 1-2 address y relative to the block's first row (rows.out).
+constexpr uint32_t kOob = 0x80000000u;  // > any block span (checked on host)
+
+template <int SM>
+__device__ __forceinline__ void tile_store(float* __restrict__ y, __amdgpu_buffer_rsrc_t rsrc,
+                                           const float* tile, const Rows& rows, int64_t t0) {
   const int c4 = (threadIdx.x & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
     const int r = i * (kNT / 8) + (threadIdx.x >> 3);
     const int len = rows.len[r];
     const int64_t t = t0 + c4;
-    float* dst = y + rows.out[r] + t;
     const float* s = tile + r * kRow + c4;
-    if (vec && t + 3 < len) {
-      *reinterpret_cast<float4*>(dst) = make_float4(s[0], s[1], s[2], s[3]);
+    if constexpr (SM == 0) {
+      float* dst = y + rows.out[r] + t;
+      if (t + 3 < len) {
+        *reinterpret_cast<float4*>(dst) = make_float4(s[0], s[1], s[2], s[3]);
+      } else {
+        if (t + 0 < len) dst[0] = s[0];
+        if (t + 1 < len) dst[1] = s[1];
+        if (t + 2 < len) dst[2] = s[2];
+        if (t + 3 < len) dst[3] = s[3];
+      }
+    } else if constexpr (SM == 1) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 d;
+      d.x = __float_as_uint(s[0]);
+      d.y = __float_as_uint(s[1]);
+      d.z = __float_as_uint(s[2]);
+      d.w = __float_as_uint(s[3]);
+      const uint32_t off = (t < len) ? (uint32_t)((rows.out[r] + t) * 4) : kOob;
+      __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, (int)off, 0, 0);
     } else {
-      if (t + 0 < len) dst[0] = s[0];
-      if (t + 1 < len) dst[1] = s[1];
-      if (t + 2 < len) dst[2] = s[2];
-      if (t + 3 < len) dst[3] = s[3];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t off = (t + e < len) ? (uint32_t)((rows.out[r] + t + e) * 4) : kOob;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s[e]), rsrc, (int)off, 0, 0);
+      }
     }
   }
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for
+// vmcnt(0), which would drain the next tile's prefetched loads and the previous
+// tile's global stores at every barrier (gfx950 counts stores in vmcnt); here
+// only this wave's LDS traffic must be complete before the s_barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
@@ -141,9 +189,10 @@ enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
 // tile's loads in flight during the current tile's arithmetic.  Samples past a
 // row's end are zeros; their outputs are never stored.  Starts with a barrier
 // (fetch reads other threads' row descriptors) and ends with one.
-template <int S, int MODE>
+template <int S, int MODE, int VM>
 __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __restrict__ y,
-                                         float* tile, const Rows& rows, int64_t T,
+                                         __amdgpu_buffer_rsrc_t rsrc, float* tile,
+                                         const Rows& rows, int64_t T,
                                          double (&s1)[S > 0 ? S : 1],
                                          double (&s2)[S > 0 ? S : 1],
                                          double (&e)[S > 0 ? 2 * S : 1], const SosParams& p,
@@ -152,13 +201,13 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
   constexpr int D = 2 * S;
   float* my = tile + threadIdx.x * kRow;
   float4 v[kLoads];
-  __syncthreads();  // every thread's row descriptors are written
-  fetch(v, x, rows, 0, vec_x);
+  lds_barrier();  // every thread's row descriptors are written
+  fetch<(VM > 0)>(v, x, rows, 0);
   for (int64_t t0 = 0; t0 < T; t0 += kTS) {
-    __syncthreads();  // readers of the previous tile are done
-    tile_put(tile, v);
-    __syncthreads();
-    if (t0 + kTS < T) fetch(v, x, rows, t0 + kTS, vec_x);
+    lds_barrier();  // readers of the previous tile are done
+    tile_put(tile, v, rows, t0);
+    lds_barrier();
+    if (t0 + kTS < T) fetch<(VM > 0)>(v, x, rows, t0 + kTS);
     if constexpr (MODE == kStateTable) {
       const double* g = G + t0 * D;
 #pragma unroll 4
@@ -175,18 +224,18 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
       }
     }
     if constexpr (MODE == kApply) {
-      __syncthreads();
-      tile_store(y, tile, rows, t0, vec_y);
+      lds_barrier();
+      tile_store<VM>(y, rsrc, tile, rows, t0);
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // ---------------------------------------------------------------------------
 // Fused single-launch cascade: pass 1 + in-LDS carry scan + pass 2.
-// Block = 4 channels x 64 chunk lanes.  C <= kCB chunks of T samples.
+// Block = kNT/kCB channels x kCB chunk lanes.  C <= kCB chunks of T samples.
 // ---------------------------------------------------------------------------
-template <int S, bool GTAB>
+template <int S, bool GTAB, int VM, int kCB>
 __global__ __launch_bounds__(kNT) void k_iir_fused(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
     int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
@@ -207,10 +256,15 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
   const int64_t b = (int64_t)blockIdx.x * CHN + cl;
   const bool live = b < B && c < C;
   const int64_t t_begin = (int64_t)c * T;
+  const int64_t b0 = (int64_t)blockIdx.x * CHN;
   s_in[tid] = live ? b * ld_x + t_begin : 0;
-  s_out[tid] = live ? b * ld_y + t_begin : 0;
+  // VM > 0 stores through a raw buffer based at the block's first output row.
+  s_out[tid] = live ? (VM > 0 ? (b - b0) * ld_y : b * ld_y) + t_begin : 0;
   s_len[tid] = live ? (int)min(T, n - t_begin) : 0;
   const Rows rows{s_in, s_out, s_len};
+  const uint32_t span = (uint32_t)(min((int64_t)CHN, B - b0) * ld_y * 4);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(y + b0 * ld_y, 0, (int)span, 0x00020000);
 
   double s1[S], s2[S], e[D];
 #pragma unroll
@@ -220,9 +274,9 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   if constexpr (GTAB) {
-    run_pass<S, kStateTable>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+    run_pass<S, kStateTable, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
   } else {
-    run_pass<S, kStateCascade>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+    run_pass<S, kStateCascade, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       e[2 * k] = s1[k];
@@ -271,7 +325,7 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
   __syncthreads();
 
   // ---- pass 2: outputs from the carried state
-  run_pass<S, kApply>(x, y, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+  run_pass<S, kApply, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
 }
 
 // ---------------------------------------------------------------------------
@@ -313,8 +367,10 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
       s2[k] = si[2 * k + 1];
     }
   }
-  run_pass<S, APPLY ? kApply : kStateCascade>(x, y, tile, rows, T, s1, s2, e, p, nullptr,
-                                              clip, vec_x != 0, vec_y != 0);
+  // Rows span many channels here: guarded loads and stores (VM 0).
+  const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0, 0x00020000);
+  run_pass<S, APPLY ? kApply : kStateCascade, 0>(x, y, none, tile, rows, T, s1, s2, e, p,
+                                                 nullptr, clip, vec_x != 0, vec_y != 0);
   if (!APPLY && live) {
     double* eo = e_out + g * (2 * S);
 #pragma unroll
@@ -458,7 +514,7 @@ struct WsLayout {
   size_t p_off, e_off, s_off, total;
 };
 
-bool fused_ok(int S, int64_t C) { return S >= 1 && S <= 8 && S != 7 && C >= 2 && C <= kCB; }
+bool fused_ok(int S, int64_t C) { return S >= 1 && S <= 8 && S != 7 && C >= 2 && C <= kCBMax; }
 
 WsLayout ws_layout(int64_t B, int64_t n, int S, int64_t T) {
   WsLayout w{0, 0, 0, 0};
@@ -488,15 +544,34 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const std::vector<double> P = chunk_transition(p, S, T);
   for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
   const int C = (int)ceil_div(n, T);
-  constexpr int CHN = kNT / kCB;
+  // 64 chunk lanes per channel (4 channels per block) when the row splits into
+  // <= 64 chunks, else 256 (one channel per block).
+  const int CB = (C <= 64) ? 64 : 256;
+  const int CHN = kNT / CB;
   const dim3 grid((unsigned)ceil_div(B, CHN));
   TraceScope trace("iir_fused", s);
-  if (G)
-    hipLaunchKernelGGL((k_iir_fused<S, true>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, ld_y,
-                       p, sp, G, T, C, clip, vec_x, vec_y);
-  else
-    hipLaunchKernelGGL((k_iir_fused<S, false>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, ld_y,
-                       p, sp, G, T, C, clip, vec_x, vec_y);
+  // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
+  // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
+  // need every block's output span to fit a 31-bit byte offset.
+  const bool span_ok = (int64_t)CHN * ld_y * 4 < (int64_t)kOob;
+  const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
+#define DSP_FUSED_LAUNCH(GT, VMv, CBv)                                                        \
+  hipLaunchKernelGGL((k_iir_fused<S, GT, VMv, CBv>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, \
+                     ld_y, p, sp, G, T, C, clip, vec_x, vec_y)
+#define DSP_FUSED_CB(GT, VMv)          \
+  if (CB == 64) DSP_FUSED_LAUNCH(GT, VMv, 64); \
+  else DSP_FUSED_LAUNCH(GT, VMv, 256);
+  if (G) {
+    if (VMr == 1) { DSP_FUSED_CB(true, 1) }
+    else if (VMr == 2) { DSP_FUSED_CB(true, 2) }
+    else { DSP_FUSED_CB(true, 0) }
+  } else {
+    if (VMr == 1) { DSP_FUSED_CB(false, 1) }
+    else if (VMr == 2) { DSP_FUSED_CB(false, 2) }
+    else { DSP_FUSED_CB(false, 0) }
+  }
+#undef DSP_FUSED_CB
+#undef DSP_FUSED_LAUNCH
   DSP_LAUNCHED("k_iir_fused");
   return DSP_OK;
 }

@@ -1,0 +1,52 @@
+"""The N > 1 bench path on CPU: two gloo ranks run bench.timed_loop (barrier +
+sync bracketing, max-over-ranks of the elapsed time) and the channel-shard
+bookkeeping.  The GPU-side RCCL launch of bench.py uses the same harness."""
+import os
+import socket
+import time
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    from dspcore.shard import shard_ranges
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r, lr, w = bench.dist_env()
+        assert (r, lr, w) == (rank, rank, world)
+        calls = []
+        delay = 0.02 * (rank + 1)          # rank 1 is the slow one
+
+        def step():
+            calls.append(1)
+            time.sleep(delay)
+
+        elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, dist=dist)
+        lo, hi = shard_ranges(32768, world)[rank]
+        out[rank] = (elapsed, len(calls), lo, hi)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_timing_is_max_over_ranks():
+    world = 2
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+    e0, n0, lo0, hi0 = out[0]
+    e1, n1, lo1, hi1 = out[1]
+    assert n0 == n1 == 5                       # warmup + timed steps on every rank
+    assert e0 == pytest.approx(e1)             # both report the max over ranks
+    assert e0 >= 3 * 0.04 * 0.95               # ... which is the slow rank's time
+    assert (lo0, hi0, lo1, hi1) == (0, 16384, 16384, 32768)

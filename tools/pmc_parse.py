@@ -1,0 +1,63 @@
+"""Summarises rocprofv3 --pmc CSV passes per kernel (mean over dispatches).
+
+HBM traffic per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half
+the bytes of a 16-B-per-lane coalesced stream on gfx950, so
+    traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes.
+Writes profiles/pmc_traffic.json (read by bench.py) when given --write."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+SHORT = [("k_src", "src_poly"), ("k_iir_fused", "iir_fused"), ("k_iir_pass<", "iir_pass"),
+         ("k_iir_carry", "iir_carry"), ("k_iir_prep", "iir_prep"), ("k_spectrum", "spectrum"),
+         ("k_fft_c2c", "fft")]
+
+
+def short(name):
+    for key, s in SHORT:
+        if key in name:
+            if s == "iir_pass":
+                return "iir_apply" if "true" in name.split("k_iir_pass<")[1][:12] else "iir_state"
+            return s
+    return None
+
+
+def main(root, write=False):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row.get("Kernel_Name", ""))
+                if k:
+                    vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    for k in sorted(vals):
+        c = {n: sum(v) / len(v) for n, v in vals[k].items()}
+        out[k] = c
+        print(f"== {k}")
+        for n in sorted(c):
+            print(f"   {n:28s} {c[n]:.6g}")
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            t = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            c["traffic_bytes"] = t
+            print(f"   traffic (2*FETCH+WRITE)     {t / 1e9:.4f} GB per launch")
+    if write:
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_traffic.json")
+        data = {}
+        if os.path.exists(path):
+            with open(path) as fh:
+                data = json.load(fh)
+        data["config3"] = {k: round(c["traffic_bytes"]) for k, c in out.items() if "traffic_bytes" in c}
+        with open(path, "w") as fh:
+            json.dump(data, fh, indent=1)
+        print("wrote", path)
+    return out
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], "--write" in sys.argv)
