@@ -104,10 +104,17 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                               window, twiddles, static_cast<hipStream_t>(stream));
 }
 
-int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
-                  int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
-                  const float* taps, int32_t K, int32_t L, int32_t M,
-                  int64_t c_offset, const double* sos_host, int32_t S,
+size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
+  const size_t cascade = dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+  if (B <= 0 || n_out <= 0 || S <= 0 || chunk_len <= 0) return cascade;
+  const int64_t C = dsp::ceil_div(n_out, chunk_len);
+  const size_t states = (size_t)B * (size_t)(C > 1 ? C - 1 : 0) * 2 * (size_t)S * sizeof(double);
+  return cascade > states ? cascade : states;
+}
+
+int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int64_t n_in,
+                  int64_t ld_x, int64_t n_out, int64_t ld_y, const float* taps, int32_t K,
+                  int32_t L, int32_t M, int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
                   int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
@@ -115,13 +122,14 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
   dsp::clear_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
+  if (B == 0) return DSP_OK;
   int rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
   if (rc) return rc;
   rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
                           state_table, workspace, workspace_bytes, s);
   if (rc) return rc;
-  return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag,
-                              window, twiddles, s);
+  return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
+                              twiddles, s);
 }
 
 int dsp_trace_enable(int32_t enable) {

@@ -80,5 +80,11 @@ int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
+// Fused cascade whose chunk end states E[B][C-1][2S] were produced upstream.
+int fused_cascade_ok(int S, int64_t n, int64_t chunk_len);
+int launch_biquad_from_states(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                              int64_t ld_y, const double* sos, int S, int clip,
+                              int64_t chunk_len, const double* E, hipStream_t s);
+
 
 }  // namespace dsp

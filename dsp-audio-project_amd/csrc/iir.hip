@@ -235,7 +235,9 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 // Fused single-launch cascade: pass 1 + in-LDS carry scan + pass 2.
 // Block = kNT/kCB channels x kCB chunk lanes.  C <= kCB chunks of T samples.
 // ---------------------------------------------------------------------------
-template <int S, bool GTAB, int VM, int kCB>
+// P1 (pass-1 mode): 0 = cascade run, 1 = state-response table G,
+// 2 = end states precomputed by the producer (G points to E[B][C-1][2S]).
+template <int S, int P1, int VM, int kCB>
 __global__ __launch_bounds__(kNT) void k_iir_fused(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
     int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
@@ -273,7 +275,13 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
   for (int i = 0; i < D; ++i) e[i] = 0.0;
 
   // ---- pass 1: zero-state end state of the lane's chunk
-  if constexpr (GTAB) {
+  if constexpr (P1 == 2) {
+    if (live && c + 1 < C) {
+      const double* ein = G + (b * (C - 1) + c) * D;
+#pragma unroll
+      for (int i = 0; i < D; ++i) e[i] = ein[i];
+    }
+  } else if constexpr (P1 == 1) {
     run_pass<S, kStateTable, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
   } else {
     run_pass<S, kStateCascade, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
@@ -537,8 +545,8 @@ int padded_stages(int S) {
 
 template <int S>
 int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
-              const SosParams& p, int clip, int64_t T, const double* G, int vec_x, int vec_y,
-              hipStream_t s) {
+              const SosParams& p, int clip, int64_t T, const double* G, int p1mode, int vec_x,
+              int vec_y, hipStream_t s) {
   static_assert(2 * S <= 16, "scan matrix is at most 16 x 16");
   ScanParams sp;
   const std::vector<double> P = chunk_transition(p, S, T);
@@ -549,27 +557,26 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const int CB = (C <= 64) ? 64 : 256;
   const int CHN = kNT / CB;
   const dim3 grid((unsigned)ceil_div(B, CHN));
-  TraceScope trace("iir_fused", s);
+  TraceScope trace(p1mode == 2 ? "iir_apply" : "iir_fused", s);
   // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
   // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
   // need every block's output span to fit a 31-bit byte offset.
   const bool span_ok = (int64_t)CHN * ld_y * 4 < (int64_t)kOob;
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
-#define DSP_FUSED_LAUNCH(GT, VMv, CBv)                                                        \
-  hipLaunchKernelGGL((k_iir_fused<S, GT, VMv, CBv>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, \
+#define DSP_FUSED_LAUNCH(P1v, VMv, CBv)                                                        \
+  hipLaunchKernelGGL((k_iir_fused<S, P1v, VMv, CBv>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, \
                      ld_y, p, sp, G, T, C, clip, vec_x, vec_y)
-#define DSP_FUSED_CB(GT, VMv)          \
-  if (CB == 64) DSP_FUSED_LAUNCH(GT, VMv, 64); \
-  else DSP_FUSED_LAUNCH(GT, VMv, 256);
-  if (G) {
-    if (VMr == 1) { DSP_FUSED_CB(true, 1) }
-    else if (VMr == 2) { DSP_FUSED_CB(true, 2) }
-    else { DSP_FUSED_CB(true, 0) }
-  } else {
-    if (VMr == 1) { DSP_FUSED_CB(false, 1) }
-    else if (VMr == 2) { DSP_FUSED_CB(false, 2) }
-    else { DSP_FUSED_CB(false, 0) }
-  }
+#define DSP_FUSED_CB(P1v, VMv)                   \
+  if (CB == 64) DSP_FUSED_LAUNCH(P1v, VMv, 64);  \
+  else DSP_FUSED_LAUNCH(P1v, VMv, 256);
+#define DSP_FUSED_VM(P1v)                        \
+  if (VMr == 1) { DSP_FUSED_CB(P1v, 1) }         \
+  else if (VMr == 2) { DSP_FUSED_CB(P1v, 2) }    \
+  else { DSP_FUSED_CB(P1v, 0) }
+  if (p1mode == 2) { DSP_FUSED_VM(2) }
+  else if (p1mode == 1) { DSP_FUSED_VM(1) }
+  else { DSP_FUSED_VM(0) }
+#undef DSP_FUSED_VM
 #undef DSP_FUSED_CB
 #undef DSP_FUSED_LAUNCH
   DSP_LAUNCHED("k_iir_fused");
@@ -628,12 +635,40 @@ int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
   const int64_t C = (S == 0) ? 1 : ceil_div(n, T);
   if constexpr (S >= 1 && S <= 8 && S != 7) {
     if (fused_ok(S, C))
-      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, vec_x, vec_y, s);
+      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, G ? 1 : 0, vec_x, vec_y, s);
   }
   return run_general<S>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
 }
 
 }  // namespace
+
+int fused_cascade_ok(int S, int64_t n, int64_t chunk_len) {
+  return S == padded_stages(S) && chunk_len > 0 && chunk_len % kTS == 0 &&
+         fused_ok(S, ceil_div(n, chunk_len));
+}
+
+int launch_biquad_from_states(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                              int64_t ld_y, const double* sos, int S, int clip,
+                              int64_t chunk_len, const double* E, hipStream_t s) {
+  DSP_REQUIRE(fused_cascade_ok(S, n, chunk_len), "no fused cascade for S=%d n=%lld T=%lld", S,
+              (long long)n, (long long)chunk_len);
+  DSP_REQUIRE(x && y && sos && E, "null pointer");
+  SosParams p;
+  for (int k = 0; k < DSP_MAX_STAGES; ++k)
+    for (int i = 0; i < 5; ++i) p.c[k][i] = (k < S) ? sos[5 * k + i] : (i == 0 ? 1.0 : 0.0);
+  const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
+  switch (S) {
+    case 1: return run_fused<1>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 2: return run_fused<2>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 3: return run_fused<3>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 4: return run_fused<4>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 5: return run_fused<5>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 6: return run_fused<6>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 8: return run_fused<8>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
+  }
+}
 
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len) {
   if (B <= 0 || n <= 0 || S < 0 || S > DSP_MAX_STAGES || chunk_len <= 0) return 0;

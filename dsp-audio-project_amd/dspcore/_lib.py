@@ -52,6 +52,7 @@ _SIGNATURES = {
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _c_i64,
         _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i64]),
     "dsp_trace_enable": (ctypes.c_int, [_c_i32]),
     "dsp_trace_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _c_i32]),
 }

@@ -57,8 +57,9 @@ class Chain:
         self.z = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
         self.mag = torch.empty((self.B, self.spec.n_fft // 2 + 1), dtype=torch.float32,
                                device=dev)
-        self.workspace = ops.biquad_workspace(self.B, n_out, self.sos.shape[0], dev,
-                                              self.chunk_len)
+        ws_bytes = _lib.load().dsp_chain_workspace_bytes(self.B, n_out, self.sos.shape[0],
+                                                         self.chunk_len)
+        self.workspace = torch.empty(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
         self.table = ops.state_table(self.sos, self.chunk_len, dev) if use_table else None
 
     # -- algorithmic traffic ---------------------------------

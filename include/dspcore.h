@@ -116,8 +116,11 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   z   = clip(cascade(y))           (dsp_biquad_cascade_f32; S == 0 and
  *                                     clip == 0 is the EQ bypass: z := y)
  *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
- * y and z must not alias.  workspace_bytes >= dsp_biquad_workspace_bytes().
+ * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes().
+ * Each row's result is bitwise independent of B.
  * ------------------------------------------------------------------------- */
+size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S,
+                                 int64_t chunk_len);
 int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
                   const float* taps, int32_t K, int32_t L, int32_t M,

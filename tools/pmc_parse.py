@@ -12,7 +12,7 @@ import re
 import sys
 from collections import defaultdict
 
-SHORT = [("k_src", "src_poly"), ("k_iir_fused", "iir_fused"), ("k_iir_pass<", "iir_pass"),
+SHORT = [("k_src_state", "src_state"), ("k_src", "src_poly"), ("k_iir_fused<6, 2", "iir_apply"), ("k_iir_fused", "iir_fused"), ("k_iir_pass<", "iir_pass"),
          ("k_iir_carry", "iir_carry"), ("k_iir_prep", "iir_prep"), ("k_spectrum", "spectrum"),
          ("k_fft_c2c", "fft")]
 
