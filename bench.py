@@ -138,6 +138,7 @@ def kernel_bytes(chain, name):
         "iir_carry": 8 * 2 * S * B * (2 * C - 1),
         "iir_apply": 8 * B * n_out + 8 * 2 * S * B * C,
         "iir_fused": 8 * B * n_out,
+        "iir_xstate": 8 * B * n_out,
         "iir_prep": 8 * (2 * S) ** 2,
         "spectrum": 4 * B * (chain.spec.seg_len + N // 2 + 1),
     }.get(name, 0)

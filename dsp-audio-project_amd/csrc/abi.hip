@@ -58,7 +58,7 @@ void clear_error() { g_error.clear(); }
 
 extern "C" {
 
-int dsp_version(void) { return 10000; /* 1.0.0 */ }
+int dsp_version(void) { return 10100; /* 1.1.0 */ }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
 
@@ -105,28 +105,36 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
 }
 
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
-  const size_t cascade = dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
-  if (B <= 0 || n_out <= 0 || S <= 0 || chunk_len <= 0) return cascade;
-  const int64_t C = dsp::ceil_div(n_out, chunk_len);
-  const size_t states = (size_t)B * (size_t)(C > 1 ? C - 1 : 0) * 2 * (size_t)S * sizeof(double);
-  return cascade > states ? cascade : states;
+  return dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+}
+
+int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
+                              int64_t c_offset, int64_t* shift, int64_t* q0, int64_t* rows) {
+  dsp::clear_error();
+  if (!shift || !q0 || !rows) return dsp::set_error(DSP_EINVAL, "null output pointer");
+  return dsp::xstate_geometry(chunk_len, K, L, M, c_offset, shift, q0, rows);
 }
 
 int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int64_t n_in,
                   int64_t ld_x, int64_t n_out, int64_t ld_y, const float* taps, int32_t K,
                   int32_t L, int32_t M, int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
-                  int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
-                  const float* window, const float* twiddles, void* workspace,
-                  size_t workspace_bytes, void* stream) {
+                  const double* xstate_table, int64_t xstate_rows, int64_t seg_start,
+                  int64_t seg_len, int32_t log2n, int64_t ld_mag, const float* window,
+                  const float* twiddles, void* workspace, size_t workspace_bytes,
+                  void* stream) {
   dsp::clear_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
   if (B == 0) return DSP_OK;
   int rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
   if (rc) return rc;
-  rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
-                          state_table, workspace, workspace_bytes, s);
+  if (xstate_table && S > 0)
+    rc = dsp::launch_biquad_xstate(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len, x,
+                                   n_in, ld_x, K, L, M, c_offset, xstate_table, xstate_rows, s);
+  else
+    rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
+                            state_table, workspace, workspace_bytes, s);
   if (rc) return rc;
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
                               twiddles, s);

@@ -66,6 +66,13 @@ inline int allow_lds(Kern kernel, size_t bytes) {
   return DSP_OK;
 }
 
+// Workgroup barrier that waits only for LDS traffic.  __syncthreads() also
+// drains outstanding global loads/stores (vmcnt(0)) on gfx950, which would
+// serialise prefetches and stores with the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Internal launchers shared by the entry points and the fused chain.
 int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
                int64_t n_out, int64_t ld_y, const float* taps, int K, int L,
@@ -81,10 +88,13 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 // Fused cascade whose chunk end states E[B][C-1][2S] were produced upstream.
-int fused_cascade_ok(int S, int64_t n, int64_t chunk_len);
-int launch_biquad_from_states(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
-                              int64_t ld_y, const double* sos, int S, int clip,
-                              int64_t chunk_len, const double* E, hipStream_t s);
-
+// Chain fast path: pass 1 of the fused cascade reads the SRC input xs through
+// the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).
+int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
+                    int64_t* q0, int64_t* rows);
+int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                         int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
+                         const float* xs, int64_t n_in, int64_t ld_xs, int K, int L, int M,
+                         int64_t c, const double* gx, int64_t gx_rows, hipStream_t s);
 
 }  // namespace dsp

@@ -1,163 +1,305 @@
-// Batched radix-2 decimation-in-time FFT and windowed magnitude spectrum for
-// gfx950, one LDS-resident transform per workgroup.
+// Batched FFT and windowed magnitude spectrum for gfx950: Stockham autosort
+// passes of radix 16 held in registers, one LDS exchange per pass.
 //
 // Replaces reference modules/dsp_core.py:41-66 (fft_diezmado_en_tiempo, a
 // recursive radix-2 DIT in pure Python: 2N-1 calls, each building exp(-2j*pi*k/N)
 // and concatenating E + W*O, E - W*O) and dsp_core.py:74-98
 // (calcular_espectro_magnitud: centre segment or zero-padded input, Hann window,
-// FFT, |X[k]| for k <= N/2).
+// FFT, |X[k]| for k <= N/2).  The DFT it computes is the same (natural-order
+// X[k] = sum_n x[n] W_N^(nk)); only the factorisation differs.
 //
-// The recursion unrolls to the classic iterative form: load the input in
-// bit-reversed order, then log2(N) butterfly stages of span 1, 2, 4, ... with
-// twiddles W_N^(k*N/2^s); that is exactly the reference's concatenation order, so
-// the output is in natural order.  All stages run in LDS: the data (N complex64,
-// padded one slot per 32 rows so the bit-reversed scatter is conflict-free) and
-// the N/2 twiddles (an fp64-computed table rounded to fp32, staged once per
-// block for N <= 2^13; read through the cache for 2^14).  HBM traffic: the input
-// segment once, the spectrum once.
+// Algorithm (per transform of N = 2^log2n points):
+//   passes p = 0..P-1 with radices R_p (16, except a first pass of 2, 4 or 8
+//   when log2n is not a multiple of 4) and Ns = R_0 * ... * R_(p-1):
+//     for every butterfly j < N/R_p, with m = j mod Ns:
+//       v[r] = in[j + r*N/R_p] * W_N^(m*r*N/(Ns*R_p))      r < R_p
+//       v    = DFT_R(v)                                    (registers)
+//       out[(j - m)*R_p + m + r*Ns] = v[r]
+//   The output is in natural order after the last pass (Stockham autosort).
+// A radix-16 pass is a 4 x 4 split with compile-time W_16 constants, so a
+// 4096-point transform is 3 LDS round trips instead of the 12 stages of a
+// radix-2 kernel.  The first pass reads HBM directly (window and zero padding
+// applied on load) and the last pass writes HBM directly (index j + r*Ns:
+// coalesced), so the transform touches LDS P-1 times.
+//
+// LDS: one padded buffer per transform, element i at i + (i >> 4): pass-0
+// writes (stride R) and the strided reads then spread over the 64 banks.
+// Twiddles: w1 = W_N^(m*N/(Ns*R)) from the caller's fp64-computed table
+// exp(-2*pi*i*k/N), k < N/2 (rounded to fp32), and w_r = w1^r by at most four
+// complex products (error ~4 ulp, far inside the 1e-5 tolerance).
+// Small transforms (N < 4096) pack 256 / (N/16) transforms per workgroup.
 #include "common.h"
 
 namespace dsp {
 namespace {
 
-__device__ __forceinline__ unsigned bitrev(unsigned v, int log2n) {
-  return log2n == 0 ? 0u : (__brev(v) >> (32 - log2n));
+enum FftMode { kC2C = 0, kR2C = 1, kSpec = 2 };
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+  return make_float2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+  return make_float2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+  return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
 }
 
-// LDS layout: element i lives at pad(i) = i + (i >> sh), sh = max(log2n - 5, 1).
-// The bit-reversed scatter of 32 consecutive inputs then hits 32 different bank
-// pairs (N >= 1024), and butterfly partners stay contiguous within a row.
-__device__ __forceinline__ int pad_shift(int log2n) { return log2n > 6 ? log2n - 5 : 1; }
-__device__ __forceinline__ int pad(int i, int sh) { return i + (i >> sh); }
-constexpr int kTwLdsMaxLog2 = 13;  // larger transforms read twiddles through the cache
-inline size_t lds_floats2(int log2n) {
-  const int n = 1 << log2n;
-  const int sh = log2n > 6 ? log2n - 5 : 1;
-  const size_t tw = log2n <= kTwLdsMaxLog2 ? (size_t)(n > 1 ? n / 2 : 1) : 0;
-  return (size_t)n + (size_t)(n >> sh) + tw;  // data + twiddles
-}
-
-// Copies the N/2 twiddles into LDS (float4 = two twiddles per load).
-__device__ __forceinline__ void load_twiddles(float2* __restrict__ stw,
-                                              const float2* __restrict__ tw, int log2n) {
-  const int half_n = (1 << log2n) >> 1;
-  if (half_n >= 2) {
-    const float4* t4 = reinterpret_cast<const float4*>(tw);
-    float4* s4 = reinterpret_cast<float4*>(stw);
-    for (int i = threadIdx.x; i < half_n / 2; i += blockDim.x) s4[i] = t4[i];
-  } else if (half_n == 1 && threadIdx.x == 0) {
-    stw[0] = tw[0];
+// a * W_16^q for a compile-time q (after unrolling); exact for q % 4 == 0.
+__device__ __forceinline__ float2 w16mul(float2 a, int q) {
+  constexpr float c1 = 0.92387953251128674f;  // cos(pi/8)
+  constexpr float s1 = 0.38268343236508977f;  // sin(pi/8)
+  constexpr float h = 0.70710678118654752f;   // sqrt(1/2)
+  switch (q & 15) {
+    case 0: return a;
+    case 1: return cmul(a, make_float2(c1, -s1));
+    case 2: return cmul(a, make_float2(h, -h));
+    case 3: return cmul(a, make_float2(s1, -c1));
+    case 4: return make_float2(a.y, -a.x);
+    case 5: return cmul(a, make_float2(-s1, -c1));
+    case 6: return cmul(a, make_float2(-h, -h));
+    case 7: return cmul(a, make_float2(-c1, -s1));
+    case 8: return make_float2(-a.x, -a.y);
+    case 9: return cmul(a, make_float2(-c1, s1));
+    case 10: return cmul(a, make_float2(-h, h));
+    case 11: return cmul(a, make_float2(-s1, c1));
+    case 12: return make_float2(-a.y, a.x);
+    case 13: return cmul(a, make_float2(s1, c1));
+    case 14: return cmul(a, make_float2(h, h));
+    default: return cmul(a, make_float2(c1, s1));
   }
 }
 
-__device__ __forceinline__ void fft_stages(float2* __restrict__ buf, int log2n, int sh,
-                                           const float2* stw) {
-  const int half_n = (1 << log2n) >> 1;
-  for (int s = 1; s <= log2n; ++s) {
-    const int h = 1 << (s - 1);
-    const int tshift = log2n - s;
-    for (int i = threadIdx.x; i < half_n; i += blockDim.x) {
-      const int k = i & (h - 1);
-      const int j = ((i >> (s - 1)) << s) + k;
-      const float2 w = stw[k << tshift];
-      const int pj = pad(j, sh), pk = pad(j + h, sh);
-      const float2 a = buf[pj];
-      const float2 o = buf[pk];
-      const float tr = fmaf(w.x, o.x, -w.y * o.y);
-      const float ti = fmaf(w.x, o.y, w.y * o.x);
-      buf[pj] = make_float2(a.x + tr, a.y + ti);
-      buf[pk] = make_float2(a.x - tr, a.y - ti);
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+  const float2 t2 = cadd(a1, a3), d = csub(a1, a3);
+  const float2 t3 = make_float2(d.y, -d.x);  // (a1 - a3) * (-i)
+  a0 = cadd(t0, t2);
+  a1 = cadd(t1, t3);
+  a2 = csub(t0, t2);
+  a3 = csub(t1, t3);
+}
+
+// In-place forward DFT of R points, natural order in and out.
+template <int R>
+__device__ __forceinline__ void dft(float2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const float2 a = v[0];
+    v[0] = cadd(a, v[1]);
+    v[1] = csub(a, v[1]);
+  } else if constexpr (R == 4) {
+    dft4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (R == 8) {
+    // n = 2 n1 + n2, k = k1 + 4 k2
+    dft4(v[0], v[2], v[4], v[6]);
+    dft4(v[1], v[3], v[5], v[7]);
+    float2 o[8];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      const float2 y0 = v[2 * k1], y1 = w16mul(v[2 * k1 + 1], 2 * k1);
+      o[k1] = cadd(y0, y1);
+      o[k1 + 4] = csub(y0, y1);
     }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = o[i];
+  } else if constexpr (R == 16) {
+    // n = 4 n1 + n2, k = k1 + 4 k2
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+    // Y[n2][k1] sits at v[4 k1 + n2]
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1)
+#pragma unroll
+      for (int n2 = 1; n2 < 4; ++n2) v[4 * k1 + n2] = w16mul(v[4 * k1 + n2], n2 * k1);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    float2 o[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) o[k1 + 4 * k2] = v[4 * k1 + k2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = o[i];
   }
 }
 
-__global__ __launch_bounds__(1024) void k_spectrum(
-    const float* __restrict__ x, float* __restrict__ mag, int64_t ld_x,
-    int64_t seg_start, int64_t seg_len, int log2n, int64_t ld_mag,
-    const float* __restrict__ win, const float2* __restrict__ tw) {
-  extern __shared__ __attribute__((aligned(16))) float2 buf[];
-  const int N = 1 << log2n;
-  const int sh = pad_shift(log2n);
-  float2* stw = buf + (N + (N >> sh) + 1) / 2 * 2;  // 16-byte aligned
-  const int64_t b = blockIdx.x;
-  const float* xr = x + b * ld_x + seg_start;
-  const bool tw_lds = log2n <= kTwLdsMaxLog2;
-  if (tw_lds) load_twiddles(stw, tw, log2n);
-  const float2* twp = tw_lds ? stw : tw;
-  // Loads are issued 4 rows at a time with clamped (always valid) addresses
-  // and masked afterwards, so they overlap instead of waiting one by one.
-  if (seg_len > 0) {
-    const int last = (int)seg_len - 1;
-    for (int n0 = threadIdx.x; n0 < N; n0 += 4 * blockDim.x) {
-      float a[4], w[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + r * blockDim.x;
-        const int nc = n < N ? n : N - 1;
-        a[r] = xr[nc < last ? nc : last];
-        w[r] = win[nc];
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + r * blockDim.x;
-        if (n < N)
-          buf[pad((int)bitrev((unsigned)n, log2n), sh)] =
-              make_float2(n < seg_len ? a[r] * w[r] : 0.f, 0.f);
-      }
-    }
+// ---------------------------------------------------------------------------
+// Compile-time plan
+// ---------------------------------------------------------------------------
+template <int LOG2N>
+struct Plan {
+  static constexpr int N = 1 << LOG2N;
+  static constexpr int NP = LOG2N == 0 ? 0 : (LOG2N + 3) / 4;
+  static constexpr int RMAX = LOG2N >= 4 ? 16 : N;
+  static constexpr int TPT = N / RMAX;                      // threads per transform
+  static constexpr int TPB = TPT >= 256 ? 1 : 256 / TPT;    // transforms per block
+  static constexpr int NT = TPB * TPT;
+  static constexpr int PADN = N + (N >> 4);
+  static constexpr int radix(int p) {
+    return (p == 0 && (LOG2N & 3) != 0) ? (1 << (LOG2N & 3)) : RMAX;
+  }
+  static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
+};
+
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+
+struct FftArgs {
+  const float* in;     // real rows (kR2C, kSpec) or interleaved complex rows (kC2C)
+  float* out;          // complex rows (kC2C, kR2C) or magnitudes (kSpec)
+  int64_t B, ld_in, ld_out;
+  int64_t seg_start, seg_len;  // kSpec
+  const float* win;            // kSpec
+  const float2* tw;            // exp(-2 pi i k / N), k < N/2
+};
+
+// Value n of transform t as the first pass reads it.
+template <int MODE>
+__device__ __forceinline__ float2 load_input(const FftArgs& a, int64_t t, int n, bool live) {
+  if (!live) return make_float2(0.f, 0.f);
+  if constexpr (MODE == kC2C) {
+    return reinterpret_cast<const float2*>(a.in)[t * a.ld_in + n];
+  } else if constexpr (MODE == kR2C) {
+    return make_float2(a.in[t * a.ld_in + n], 0.f);
   } else {
-    for (int n = threadIdx.x; n < N; n += blockDim.x) buf[pad(n, sh)] = make_float2(0.f, 0.f);
-  }
-  __syncthreads();
-  fft_stages(buf, log2n, sh, twp);
-  float* mr = mag + b * ld_mag;
-  for (int k = threadIdx.x; k <= (N >> 1); k += blockDim.x) {
-    const float2 v = buf[pad(k, sh)];
-    mr[k] = sqrtf(fmaf(v.x, v.x, v.y * v.y));
+    const float s = (n < a.seg_len) ? a.in[t * a.ld_in + a.seg_start + n] : 0.f;
+    return make_float2(s * a.win[n], 0.f);
   }
 }
 
-__global__ __launch_bounds__(1024) void k_fft_c2c(
-    const float* __restrict__ in, float* __restrict__ out, int log2n,
-    int real_in, int64_t ld_in, int64_t ld_out, const float2* __restrict__ tw) {
-  extern __shared__ __attribute__((aligned(16))) float2 buf[];
-  const int N = 1 << log2n;
-  const int sh = pad_shift(log2n);
-  float2* stw = buf + (N + (N >> sh) + 1) / 2 * 2;
-  const int64_t b = blockIdx.x;
-  const bool tw_lds = log2n <= kTwLdsMaxLog2;
-  if (tw_lds) load_twiddles(stw, tw, log2n);
-  const float2* twp = tw_lds ? stw : tw;
-  for (int n0 = threadIdx.x; n0 < N; n0 += 4 * blockDim.x) {
-    float2 a[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + r * blockDim.x;
-      const int nc = n < N ? n : N - 1;
-      if (real_in)
-        a[r] = make_float2(in[b * ld_in + nc], 0.f);
-      else
-        a[r] = reinterpret_cast<const float2*>(in)[b * ld_in + nc];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + r * blockDim.x;
-      if (n < N) buf[pad((int)bitrev((unsigned)n, log2n), sh)] = a[r];
-    }
+template <int MODE, int N>
+__device__ __forceinline__ void store_output(const FftArgs& a, int64_t t, int k, float2 v,
+                                             bool live) {
+  if (!live) return;
+  if constexpr (MODE == kSpec) {
+    if (k <= N / 2) a.out[t * a.ld_out + k] = sqrtf(fmaf(v.x, v.x, v.y * v.y));
+  } else {
+    reinterpret_cast<float2*>(a.out)[t * a.ld_out + k] = v;
   }
-  __syncthreads();
-  fft_stages(buf, log2n, sh, twp);
-  float2* yr = reinterpret_cast<float2*>(out) + b * ld_out;
-  for (int n = threadIdx.x; n < N; n += blockDim.x) yr[n] = buf[pad(n, sh)];
 }
 
-int threads_for(int log2n) {
-  const int half_n = (1 << log2n) >> 1;
-  int nt = half_n < 64 ? 64 : half_n;
-  if (nt > 256 && log2n <= 12) nt = 256;
-  if (nt > 1024) nt = 1024;
-  return nt;
+// w1 of every butterfly of pass P (the twiddle loads are issued before pass 0 so
+// their latency hides under it instead of after each barrier).
+template <int LOG2N, int P>
+struct Tw {
+  float2 w[Plan<LOG2N>::NP > P + 1 ? Plan<LOG2N>::RMAX / Plan<LOG2N>::radix(P + 1) : 1];
+  Tw<LOG2N, P + 1> next;
+};
+template <int LOG2N>
+struct Tw<LOG2N, 15> {};
+
+template <int LOG2N, int P>
+__device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restrict__ table,
+                                        int j0) {
+  using PL = Plan<LOG2N>;
+  if constexpr (P + 1 < PL::NP) {
+    constexpr int R = PL::radix(P + 1);
+    constexpr int NS = PL::ns(P + 1);
+#pragma unroll
+    for (int b = 0; b < PL::RMAX / R; ++b) {
+      const int m = (j0 + b * PL::TPT) & (NS - 1);
+      tw.w[b] = table[m * (PL::N / (NS * R))];
+    }
+    load_tw<LOG2N, P + 1>(tw.next, table, j0);
+  }
+}
+
+template <int LOG2N, int MODE, int P>
+__device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t t, int j0,
+                                         bool live, const Tw<LOG2N, P - 1 < 0 ? 0 : P - 1>& tw) {
+  using PL = Plan<LOG2N>;
+  constexpr int N = PL::N;
+  constexpr int R = PL::radix(P);
+  constexpr int NS = PL::ns(P);
+  constexpr int NB = PL::RMAX / R;  // butterflies per thread
+  constexpr int STRIDE = N / R;
+  constexpr bool FIRST = P == 0, LAST = P == PL::NP - 1;
+  float2 v[NB][R];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = j0 + b * PL::TPT;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int n = j + r * STRIDE;
+      v[b][r] = FIRST ? load_input<MODE>(a, t, n, live) : buf[lpad(n)];
+    }
+  }
+  if constexpr (!FIRST) __syncthreads();  // every read of this pass precedes its writes
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = j0 + b * PL::TPT;
+    const int m = j & (NS - 1);
+    if constexpr (NS > 1) {
+      float2 w[R];
+      w[1] = tw.w[b];
+#pragma unroll
+      for (int r = 2; r < R; ++r) w[r] = (r & 1) ? cmul(w[r - 1], w[1]) : cmul(w[r / 2], w[r / 2]);
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[r]);
+    }
+    dft<R>(v[b]);
+    const int base = (j - m) * R + m;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = base + r * NS;
+      if constexpr (LAST) store_output<MODE, N>(a, t, k, v[b][r], live);
+      else buf[lpad(k)] = v[b][r];
+    }
+  }
+  if constexpr (!LAST) __syncthreads();
+  if constexpr (P + 1 < PL::NP) {
+    if constexpr (P == 0) run_pass<LOG2N, MODE, P + 1>(a, buf, t, j0, live, tw);
+    else run_pass<LOG2N, MODE, P + 1>(a, buf, t, j0, live, tw.next);
+  }
+}
+
+template <int LOG2N, int MODE>
+__global__ __launch_bounds__(Plan<LOG2N>::NT) void k_fft(FftArgs a) {
+  using PL = Plan<LOG2N>;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int tl = threadIdx.x / PL::TPT;
+  const int j0 = threadIdx.x - tl * PL::TPT;
+  const int64_t t = (int64_t)blockIdx.x * PL::TPB + tl;
+  const bool live = t < a.B;
+  if constexpr (PL::NP == 0) {
+    store_output<MODE, 1>(a, t, 0, load_input<MODE>(a, t, 0, live), live);
+  } else {
+    Tw<LOG2N, 0> tw;
+    load_tw<LOG2N, 0>(tw, a.tw, j0);
+    run_pass<LOG2N, MODE, 0>(a, lds + tl * PL::PADN, t, j0, live, tw);
+  }
+}
+
+template <int MODE, int LOG2N>
+int launch_one(const FftArgs& a, hipStream_t s) {
+  using PL = Plan<LOG2N>;
+  const size_t shm = (size_t)PL::TPB * PL::PADN * sizeof(float2);
+  if (int rc = allow_lds(k_fft<LOG2N, MODE>, shm)) return rc;
+  const unsigned grid = (unsigned)ceil_div(a.B, PL::TPB);
+  hipLaunchKernelGGL((k_fft<LOG2N, MODE>), dim3(grid), dim3(PL::NT), shm, s, a);
+  DSP_LAUNCHED("k_fft");
+  return DSP_OK;
+}
+
+template <int MODE>
+int dispatch(const FftArgs& a, int log2n, hipStream_t s) {
+  switch (log2n) {
+    case 0: return launch_one<MODE, 0>(a, s);
+    case 1: return launch_one<MODE, 1>(a, s);
+    case 2: return launch_one<MODE, 2>(a, s);
+    case 3: return launch_one<MODE, 3>(a, s);
+    case 4: return launch_one<MODE, 4>(a, s);
+    case 5: return launch_one<MODE, 5>(a, s);
+    case 6: return launch_one<MODE, 6>(a, s);
+    case 7: return launch_one<MODE, 7>(a, s);
+    case 8: return launch_one<MODE, 8>(a, s);
+    case 9: return launch_one<MODE, 9>(a, s);
+    case 10: return launch_one<MODE, 10>(a, s);
+    case 11: return launch_one<MODE, 11>(a, s);
+    case 12: return launch_one<MODE, 12>(a, s);
+    case 13: return launch_one<MODE, 13>(a, s);
+    case 14: return launch_one<MODE, 14>(a, s);
+    default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N);
+  }
 }
 
 }  // namespace
@@ -176,15 +318,10 @@ int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
   DSP_REQUIRE(ld_x >= seg_start + seg_len, "segment exceeds the row");
   if (B == 0) return DSP_OK;
   DSP_REQUIRE(x && mag && window && tw, "null pointer");
-  const size_t shm = (lds_floats2(log2n) + 2) * sizeof(float2);
-  if (shm > 160 * 1024) return set_error(DSP_ENOTSUP, "FFT of 2^%d does not fit in LDS", log2n);
-  if (int rc = allow_lds(k_spectrum, shm)) return rc;
+  FftArgs a{x, mag, B, ld_x, ld_mag, seg_start, seg_len, window,
+            reinterpret_cast<const float2*>(tw)};
   TraceScope trace("spectrum", s);
-  hipLaunchKernelGGL(k_spectrum, dim3((unsigned)B), dim3(threads_for(log2n)), shm, s, x,
-                     mag, ld_x, seg_start, seg_len, log2n, ld_mag, window,
-                     reinterpret_cast<const float2*>(tw));
-  DSP_LAUNCHED("k_spectrum");
-  return DSP_OK;
+  return dispatch<kSpec>(a, log2n, s);
 }
 
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
@@ -198,15 +335,9 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
                   (real_in || (reinterpret_cast<uintptr_t>(in) & 7) == 0),
               "complex buffers must be 8-byte aligned");
-  const size_t shm = (lds_floats2(log2n) + 2) * sizeof(float2);
-  if (shm > 160 * 1024) return set_error(DSP_ENOTSUP, "FFT of 2^%d does not fit in LDS", log2n);
-  if (int rc = allow_lds(k_fft_c2c, shm)) return rc;
+  FftArgs a{in, out, B, ld_in, ld_out, 0, 0, nullptr, reinterpret_cast<const float2*>(tw)};
   TraceScope trace("fft", s);
-  hipLaunchKernelGGL(k_fft_c2c, dim3((unsigned)B), dim3(threads_for(log2n)), shm, s, in,
-                     out, log2n, real_in, ld_in, ld_out,
-                     reinterpret_cast<const float2*>(tw));
-  DSP_LAUNCHED("k_fft_c2c");
-  return DSP_OK;
+  return real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s);
 }
 
 }  // namespace dsp

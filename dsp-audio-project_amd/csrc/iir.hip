@@ -17,17 +17,19 @@
 //   pass 1: chunk end state from zero state, E_c = sum_n A^(T-1-n) B u[n]
 //           - either by running the cascade (~30 fp64 ops per sample), or
 //           - with the caller's state-response table G[t] = A^(T-1-t) B as a
-//             2S-FMA-per-sample dot product (no recurrence, no dependency chain);
+//             2S-FMA-per-sample dot product (no recurrence, no dependency chain),
+//           - or (chain) with G composed with the SRC taps, over the SRC input;
 //   scan:   S_0 = 0, S_{c+1} = A^T S_c + E_c  (A^T is computed on the host);
 //   pass 2: rerun every chunk from S_c, clip, store.
-// With C <= 64 and S <= 8 all three run in ONE kernel (k_iir_fused): a block
-// holds every chunk of 4 channels, so the scan is an in-LDS sequence of
-// 2S-FMA row updates between pass 1 and pass 2.  Otherwise the general path
-// runs pass 1, a carry kernel and pass 2 as separate launches.  The chunking
-// depends only on the caller's chunk_len, never on B, so a row's result is
-// bitwise identical however the batch is sized or sharded.
+// With C <= 64 and S <= 8 all three run in ONE kernel (k_iir_wave): one
+// wavefront owns one channel, lane c = chunk c, so tile staging, the carry scan
+// and both passes are wave-private -- no workgroup barrier anywhere, and each
+// wave streams independently of the others on its SIMD.  Otherwise the general
+// path runs pass 1, a carry kernel and pass 2 as separate launches.  The
+// chunking depends only on the caller's chunk_len, never on B, so a row's
+// result is bitwise identical however the batch is sized or sharded.
 //
-// Memory.  Lanes are (channel, chunk) rows.  A 256-row x 32-sample fp32 tile is
+// Memory.  Lanes are (channel, chunk) rows.  An NR-row x 32-sample fp32 tile is
 // loaded with coalesced 128-byte row segments into LDS (row stride 33 floats:
 // conflict-free per-lane column reads); the next tile's global loads are issued
 // into registers before the current tile is computed, so HBM latency hides
@@ -48,11 +50,14 @@ struct ScanParams {
   double P[16 * 16];  // A^T, row-major D x D, D = 2S <= 16
 };
 
-constexpr int kNT = 256;       // lanes (rows) per block
-constexpr int kTS = 32;        // samples per tile step
+constexpr int kNT = 256;       // lanes (rows) per block, general path
+constexpr int kTS = 32;        // samples per tile step (chunk_len granule)
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
-constexpr int kCBMax = 256;    // max chunks per channel in the fused kernel
-constexpr int kLoads = kNT * kTS / 4 / kNT;  // float4 loads per thread per tile
+constexpr int kLoads = kTS / 4;  // float4 loads per thread per tile (one row per thread)
+constexpr int kCBMax = kWave;  // max chunks per channel in the fused kernel
+#ifndef DSP_IIR_EXPERIMENT
+#define DSP_IIR_EXPERIMENT 0  // 1: no arithmetic, 2: no global loads (timing only)
+#endif
 
 template <int S>
 __device__ __forceinline__ double cascade_step(double u, double (&s1)[S > 0 ? S : 1],
@@ -74,55 +79,74 @@ __device__ __forceinline__ double clip1(double v) {
 }
 
 // Row descriptors live in LDS: global offset of the row's first sample for
-// input and output, and the number of valid samples in the row.
+// input and output, and the valid sample range [lo, len) of the row.
 struct Rows {
   int64_t* in;
   int64_t* out;
   int* len;
+  int* lo;
 };
 
-// Issues this thread's kLoads float4 loads of tile [t0, t0+32) into registers.
-// VEC (rows 16-byte aligned, ld % 4 == 0): branch-free -- every vector with at
-// least one valid sample is loaded whole (ld % 4 == 0 and ld >= n keep the
-// over-read inside the row pitch), others load a dummy vector at x; masking is
-// deferred to tile_put so no wait lands between the loads and their use.
-// !VEC: guarded scalar loads (slow path for odd pitches).
-template <bool VEC>
+// Tile hand-off between the NR threads that share a tile.  NR == 64 (one
+// wave): LDS instructions of a wave execute in program order, so a compiler
+// fence suffices.  NR > 64: a workgroup barrier that waits only for LDS
+// traffic -- __syncthreads() would also wait for vmcnt(0) and drain the next
+// tile's prefetched loads and the previous tile's stores at every barrier.
+template <int NR>
+__device__ __forceinline__ void tile_sync() {
+  if constexpr (NR == kWave) {
+    asm volatile("" ::: "memory");
+  } else {
+    lds_barrier();
+  }
+}
+
+// Issues this thread's kLoads float4 loads of tile [t0, t0+32) into registers
+// (8 threads per row, 128 contiguous bytes).  tid is the thread's index among
+// the NR threads sharing the tile.
+// VEC (rows 16-byte aligned, ld % 4 == 0, lo % 4 == 0): branch-free -- every
+// vector with at least one valid sample is loaded whole (ld % 4 == 0 and
+// ld >= n keep the over-read inside the row pitch), others load a dummy vector
+// at x; masking is deferred to tile_put so no wait lands between the loads and
+// their use.  !VEC: guarded scalar loads (slow path for odd pitches).
+template <int NR, bool VEC>
 __device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restrict__ x,
-                                      const Rows& rows, int64_t t0) {
-  const int c4 = (threadIdx.x & 7) * 4;
+                                      const Rows& rows, int64_t t0, int tid) {
+  const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
-    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int r = i * (NR / 8) + (tid >> 3);
     const int len = rows.len[r];
     const int64_t t = t0 + c4;
     if constexpr (VEC) {
-      const float* src = (t < len) ? x + rows.in[r] + t : x;
+      const float* src = (t < len && t >= rows.lo[r]) ? x + rows.in[r] + t : x;
       v[i] = *reinterpret_cast<const float4*>(src);
     } else {
+      const int lo = rows.lo[r];
       const float* src = x + rows.in[r] + t;
-      v[i].x = (t + 0 < len) ? src[0] : 0.f;
-      v[i].y = (t + 1 < len) ? src[1] : 0.f;
-      v[i].z = (t + 2 < len) ? src[2] : 0.f;
-      v[i].w = (t + 3 < len) ? src[3] : 0.f;
+      v[i].x = (t + 0 < len && t + 0 >= lo) ? src[0] : 0.f;
+      v[i].y = (t + 1 < len && t + 1 >= lo) ? src[1] : 0.f;
+      v[i].z = (t + 2 < len && t + 2 >= lo) ? src[2] : 0.f;
+      v[i].w = (t + 3 < len && t + 3 >= lo) ? src[3] : 0.f;
     }
   }
 }
 
-// Writes the fetched tile into LDS, zeroing samples past each row's end.
+// Writes the fetched tile into LDS, zeroing samples outside each row's range.
+template <int NR>
 __device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads],
-                                         const Rows& rows, int64_t t0) {
-  const int c4 = (threadIdx.x & 7) * 4;
+                                         const Rows& rows, int64_t t0, int tid) {
+  const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
-    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int r = i * (NR / 8) + (tid >> 3);
     const int64_t t = t0 + c4;
-    const int len = rows.len[r];
+    const int len = rows.len[r], lo = rows.lo[r];
     float* d = tile + r * kRow + c4;
-    d[0] = (t + 0 < len) ? v[i].x : 0.f;
-    d[1] = (t + 1 < len) ? v[i].y : 0.f;
-    d[2] = (t + 2 < len) ? v[i].z : 0.f;
-    d[3] = (t + 3 < len) ? v[i].w : 0.f;
+    d[0] = (t + 0 < len && t + 0 >= lo) ? v[i].x : 0.f;
+    d[1] = (t + 1 < len && t + 1 >= lo) ? v[i].y : 0.f;
+    d[2] = (t + 2 < len && t + 2 >= lo) ? v[i].z : 0.f;
+    d[3] = (t + 3 < len && t + 3 >= lo) ? v[i].w : 0.f;
   }
 }
 
@@ -133,16 +157,17 @@ __device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads],
 //      count vmcnt exactly and the next tile's wait never drains these stores;
 //   2: like 1 with four dword stores per vector (rows whose length is not a
 //      multiple of 4 end in a partial vector).
-// Modes 1-2 address y relative to the block's first row (rows.out).
-constexpr uint32_t kOob = 0x80000000u;  // > any block span (checked on host)
+// Modes 1-2 address y relative to the buffer resource's base (rows.out).
+constexpr uint32_t kOob = 0x80000000u;  // > any buffer span (checked on host)
 
-template <int SM>
+template <int NR, int SM>
 __device__ __forceinline__ void tile_store(float* __restrict__ y, __amdgpu_buffer_rsrc_t rsrc,
-                                           const float* tile, const Rows& rows, int64_t t0) {
-  const int c4 = (threadIdx.x & 7) * 4;
+                                           const float* tile, const Rows& rows, int64_t t0,
+                                           int tid) {
+  const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
-    const int r = i * (kNT / 8) + (threadIdx.x >> 3);
+    const int r = i * (NR / 8) + (tid >> 3);
     const int len = rows.len[r];
     const int64_t t = t0 + c4;
     const float* s = tile + r * kRow + c4;
@@ -175,40 +200,45 @@ __device__ __forceinline__ void tile_store(float* __restrict__ y, __amdgpu_buffe
   }
 }
 
-// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for
-// vmcnt(0), which would drain the next tile's prefetched loads and the previous
-// tile's global stores at every barrier (gfx950 counts stores in vmcnt); here
-// only this wave's LDS traffic must be complete before the s_barrier.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
 enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
 
-// One pass over every lane's row of T samples, tile by tile, with the next
-// tile's loads in flight during the current tile's arithmetic.  Samples past a
-// row's end are zeros; their outputs are never stored.  Starts with a barrier
-// (fetch reads other threads' row descriptors) and ends with one.
-template <int S, int MODE, int VM>
+// One pass over every row of the NR-row group, tile by tile, with the next
+// tile's loads in flight during the current tile's arithmetic.  Samples outside
+// a row's range are zeros; their outputs are never stored.  Starts with a
+// hand-off (fetch reads other threads' row descriptors) and ends with one.
+template <int S, int MODE, int NR, int VM, bool VIN>
 __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __restrict__ y,
                                          __amdgpu_buffer_rsrc_t rsrc, float* tile,
-                                         const Rows& rows, int64_t T,
+                                         const Rows& rows, int64_t T, int tid,
                                          double (&s1)[S > 0 ? S : 1],
                                          double (&s2)[S > 0 ? S : 1],
                                          double (&e)[S > 0 ? 2 * S : 1], const SosParams& p,
-                                         const double* __restrict__ G, int clip, bool vec_x,
-                                         bool vec_y) {
+                                         const double* __restrict__ G, int clip) {
   constexpr int D = 2 * S;
-  float* my = tile + threadIdx.x * kRow;
+  float* my = tile + tid * kRow;
   float4 v[kLoads];
-  lds_barrier();  // every thread's row descriptors are written
-  fetch<(VM > 0)>(v, x, rows, 0);
+  tile_sync<NR>();  // every thread's row descriptors are written
+#if DSP_IIR_EXPERIMENT == 2 || DSP_IIR_EXPERIMENT == 4
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) v[i] = make_float4(0.25f, -0.5f, 0.125f, 0.75f);
+#else
+  fetch<NR, VIN>(v, x, rows, 0, tid);
+#endif
   for (int64_t t0 = 0; t0 < T; t0 += kTS) {
-    lds_barrier();  // readers of the previous tile are done
-    tile_put(tile, v, rows, t0);
-    lds_barrier();
-    if (t0 + kTS < T) fetch<(VM > 0)>(v, x, rows, t0 + kTS);
+    tile_sync<NR>();  // readers of the previous tile are done
+    tile_put<NR>(tile, v, rows, t0, tid);
+    tile_sync<NR>();
+#if DSP_IIR_EXPERIMENT != 2 && DSP_IIR_EXPERIMENT != 4
+    if (t0 + kTS < T) fetch<NR, VIN>(v, x, rows, t0 + kTS, tid);
+#endif
+#if DSP_IIR_EXPERIMENT == 1
+    if (MODE == kStateTable) e[0] += my[3];
+    if constexpr (MODE == kApply) {
+      if (clip == 12345) my[0] = 1.f;
+    } else if constexpr (false) {
+#else
     if constexpr (MODE == kStateTable) {
+#endif
       const double* g = G + t0 * D;
 #pragma unroll 4
       for (int j = 0; j < kTS; ++j) {
@@ -224,49 +254,71 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
       }
     }
     if constexpr (MODE == kApply) {
-      lds_barrier();
-      tile_store<VM>(y, rsrc, tile, rows, t0);
+      tile_sync<NR>();
+#if DSP_IIR_EXPERIMENT == 3 || DSP_IIR_EXPERIMENT == 4
+      if (clip == 12345)
+#endif
+      tile_store<NR, VM>(y, rsrc, tile, rows, t0, tid);
     }
   }
-  lds_barrier();
+  tile_sync<NR>();
 }
 
 // ---------------------------------------------------------------------------
-// Fused single-launch cascade: pass 1 + in-LDS carry scan + pass 2.
-// Block = kNT/kCB channels x kCB chunk lanes.  C <= kCB chunks of T samples.
+// Fused single-launch cascade: pass 1 + carry scan + pass 2, one wavefront per
+// channel, lane c = chunk c (C <= 64 chunks of T samples).
 // ---------------------------------------------------------------------------
-// P1 (pass-1 mode): 0 = cascade run, 1 = state-response table G,
-// 2 = end states precomputed by the producer (G points to E[B][C-1][2S]).
-template <int S, int P1, int VM, int kCB>
-__global__ __launch_bounds__(kNT) void k_iir_fused(
+// P1 (pass-1 mode): 0 = cascade run over the chunk, 1 = state-response table
+// G[T][2S] over the chunk, 2 = state-response table projected onto the SRC
+// input (chain only): when x = SRC(xs) the end state of chunk c is
+//     E_c = sum_j Gx[j] xs[c*XS.shift + XS.q0 + j],  j < XS.rows,
+// with Gx = G composed with the polyphase taps on the host in float64
+// (dspcore/design.py:xstate_table).  Pass 1 then reads the SRC input (2/3 of
+// the bytes at L/M = 3/2) and costs 2S*M/L FMAs per output sample instead of
+// 2S, and the chunk states are those of the exact float64 SRC output.
+struct XState {
+  const float* xs;  // SRC input rows [B][ld]
+  int64_t ld, n, shift, q0, rows;
+};
+
+// Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
+constexpr int kWaveTileFloats = kWave * kRow;
+
+template <int S, int P1, int VM>
+__global__ __launch_bounds__(kWave) void k_iir_wave(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
     int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
-    const double* __restrict__ G, int64_t T, int C, int clip, int vec_x, int vec_y) {
+    const double* __restrict__ G, int64_t T, int C, int clip, XState XS) {
   constexpr int D = 2 * S;
-  constexpr int CHN = kNT / kCB;
-  constexpr int kTileBytes = kNT * kRow * 4;
-  constexpr int kScanBytes = kNT * D * 8;
-  __shared__ __attribute__((aligned(16)))
-  char smem[kTileBytes > kScanBytes ? kTileBytes : kScanBytes];
-  __shared__ int64_t s_in[kNT], s_out[kNT];
-  __shared__ int s_len[kNT];
-  float* tile = reinterpret_cast<float*>(smem);
-  double* scan = reinterpret_cast<double*>(smem);
+  static_assert(kWave * D * 2 <= kWaveTileFloats, "scan must fit in the tile");
+  __shared__ __attribute__((aligned(16))) float tile[kWaveTileFloats];
+  __shared__ int64_t s_in[kWave], s_out[kWave];
+  __shared__ int s_len[kWave], s_lo[kWave];
+  double* scan = reinterpret_cast<double*>(tile);
 
-  const int tid = threadIdx.x;
-  const int cl = tid / kCB, c = tid % kCB;
-  const int64_t b = (int64_t)blockIdx.x * CHN + cl;
-  const bool live = b < B && c < C;
+  const int c = threadIdx.x;  // chunk
+  const int64_t b = blockIdx.x;
+  const bool live = c < C;
   const int64_t t_begin = (int64_t)c * T;
-  const int64_t b0 = (int64_t)blockIdx.x * CHN;
-  s_in[tid] = live ? b * ld_x + t_begin : 0;
-  // VM > 0 stores through a raw buffer based at the block's first output row.
-  s_out[tid] = live ? (VM > 0 ? (b - b0) * ld_y : b * ld_y) + t_begin : 0;
-  s_len[tid] = live ? (int)min(T, n - t_begin) : 0;
-  const Rows rows{s_in, s_out, s_len};
-  const uint32_t span = (uint32_t)(min((int64_t)CHN, B - b0) * ld_y * 4);
+  // Pass-2 row descriptors (pass 1 of mode 2 reads other rows first).
+  const int64_t in2 = live ? b * ld_x + t_begin : 0;
+  const int len2 = live ? (int)min(T, n - t_begin) : 0;
+  if constexpr (P1 == 2) {
+    const int64_t start = (int64_t)c * XS.shift + XS.q0;  // may be < 0 for c = 0
+    const bool need = c + 1 < C;                          // last chunk: state unused
+    s_in[c] = need ? b * XS.ld + start : 0;
+    s_lo[c] = need ? (int)max((int64_t)0, -start) : 0;
+    s_len[c] = need ? (int)max((int64_t)0, min(XS.rows, XS.n - start)) : 0;
+  } else {
+    s_in[c] = in2;
+    s_lo[c] = 0;
+    s_len[c] = c + 1 < C ? len2 : 0;  // last chunk: state unused
+  }
+  // VM > 0 stores through a raw buffer based at this channel's output row.
+  s_out[c] = live ? (VM > 0 ? 0 : b * ld_y) + t_begin : 0;
+  const Rows rows{s_in, s_out, s_len, s_lo};
   const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(y + b0 * ld_y, 0, (int)span, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(y + b * ld_y, 0, (int)(n * 4), 0x00020000);
 
   double s1[S], s2[S], e[D];
 #pragma unroll
@@ -276,15 +328,14 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   if constexpr (P1 == 2) {
-    if (live && c + 1 < C) {
-      const double* ein = G + (b * (C - 1) + c) * D;
-#pragma unroll
-      for (int i = 0; i < D; ++i) e[i] = ein[i];
-    }
+    run_pass<S, kStateTable, kWave, VM, true>(XS.xs, y, rsrc, tile, rows, XS.rows, c, s1, s2,
+                                               e, p, G, clip);
   } else if constexpr (P1 == 1) {
-    run_pass<S, kStateTable, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+    run_pass<S, kStateTable, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p,
+                                                   G, clip);
   } else {
-    run_pass<S, kStateCascade, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+    run_pass<S, kStateCascade, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e,
+                                                     p, G, clip);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       e[2 * k] = s1[k];
@@ -292,48 +343,49 @@ __global__ __launch_bounds__(kNT) void k_iir_fused(
     }
   }
 
-  // ---- carry scan in LDS.  slot c holds E_c; step cc overwrites slot cc with
-  // S_{cc+1} = P S_cc + E_cc once E_cc has been consumed (S_cc sits in slot
-  // cc-1), so chunk c >= 1 finds its initial state in slot c-1.
+  // ---- carry scan: slot c holds E_c; step cc overwrites slot cc with
+  // S_{cc+1} = P S_cc + E_cc (S_cc sits in slot cc-1), so chunk c >= 1 finds
+  // its initial state in slot c-1.  Lanes 0..D-1 each own one state
+  // component; the wave's LDS instructions execute in order.
 #pragma unroll
-  for (int i = 0; i < D; ++i) scan[tid * D + i] = e[i];
-  const bool row_thread = tid < CHN * D;
-  const int rc = tid / D, ri = tid - (tid / D) * D;
+  for (int i = 0; i < D; ++i) scan[c * D + i] = e[i];
+  s_in[c] = in2;  // pass-2 rows; pass 2 opens with a hand-off
+  s_lo[c] = 0;
+  s_len[c] = len2;
+  const bool row_lane = c < D;
   double prow[D];
-  if (row_thread) {
+  if (row_lane) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) prow[j] = sp.P[ri * D + j];
+    for (int j = 0; j < D; ++j) prow[j] = sp.P[c * D + j];
   }
-  __syncthreads();
+  asm volatile("" ::: "memory");
   for (int cc = 0; cc + 1 < C; ++cc) {
-    double acc = 0.0;
-    if (row_thread) {
-      const double* cur = scan + (rc * kCB + cc) * D;
-      acc = cur[ri];
+    if (row_lane) {
+      double acc = scan[cc * D + c];
       if (cc > 0) {
-        const double* prev = cur - D;  // S_cc
 #pragma unroll
-        for (int j = 0; j < D; ++j) acc = fma(prow[j], prev[j], acc);
+        for (int j = 0; j < D; ++j) acc = fma(prow[j], scan[(cc - 1) * D + j], acc);
       }
+      asm volatile("" ::: "memory");  // all reads of S_cc precede the write
+      scan[cc * D + c] = acc;
     }
-    __syncthreads();
-    if (row_thread) scan[(rc * kCB + cc) * D + ri] = acc;
-    __syncthreads();
+    asm volatile("" ::: "memory");
   }
   if (c > 0) {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      s1[k] = scan[(tid - 1) * D + 2 * k];
-      s2[k] = scan[(tid - 1) * D + 2 * k + 1];
+      s1[k] = scan[(c - 1) * D + 2 * k];
+      s2[k] = scan[(c - 1) * D + 2 * k + 1];
     }
   } else {
 #pragma unroll
     for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
   }
-  __syncthreads();
+  asm volatile("" ::: "memory");
 
   // ---- pass 2: outputs from the carried state
-  run_pass<S, kApply, VM>(x, y, rsrc, tile, rows, T, s1, s2, e, p, G, clip, vec_x, vec_y);
+  run_pass<S, kApply, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p, G,
+                                            clip);
 }
 
 // ---------------------------------------------------------------------------
@@ -348,7 +400,7 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
   constexpr int SS = S > 0 ? S : 1;
   __shared__ __attribute__((aligned(16))) float tile[kNT * kRow];
   __shared__ int64_t s_in[kNT], s_out[kNT];
-  __shared__ int s_len[kNT];
+  __shared__ int s_len[kNT], s_lo[kNT];
   const int tid = threadIdx.x;
   const int64_t g = (int64_t)blockIdx.x * kNT + tid;
   const int64_t cl = APPLY ? C : C - 1;  // chunks per channel handled here
@@ -362,7 +414,8 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
   s_in[tid] = b * ld_x + t_begin;
   s_out[tid] = b * ld_y + t_begin;
   s_len[tid] = live ? (int)min(T, n - t_begin) : 0;
-  const Rows rows{s_in, s_out, s_len};
+  s_lo[tid] = 0;
+  const Rows rows{s_in, s_out, s_len, s_lo};
 
   double s1[SS], s2[SS], e[S > 0 ? 2 * S : 1];
 #pragma unroll
@@ -377,8 +430,12 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
   }
   // Rows span many channels here: guarded loads and stores (VM 0).
   const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0, 0x00020000);
-  run_pass<S, APPLY ? kApply : kStateCascade, 0>(x, y, none, tile, rows, T, s1, s2, e, p,
-                                                 nullptr, clip, vec_x != 0, vec_y != 0);
+  if (vec_x)
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, true>(x, y, none, tile, rows, T, tid, s1,
+                                                              s2, e, p, nullptr, clip);
+  else
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, false>(x, y, none, tile, rows, T, tid,
+                                                               s1, s2, e, p, nullptr, clip);
   if (!APPLY && live) {
     double* eo = e_out + g * (2 * S);
 #pragma unroll
@@ -522,12 +579,14 @@ struct WsLayout {
   size_t p_off, e_off, s_off, total;
 };
 
-bool fused_ok(int S, int64_t C) { return S >= 1 && S <= 8 && S != 7 && C >= 2 && C <= kCBMax; }
+bool fused_ok(int S, int64_t C, int64_t T) {
+  return S >= 1 && S <= 8 && S != 7 && C >= 2 && C <= kCBMax && T % kTS == 0;
+}
 
 WsLayout ws_layout(int64_t B, int64_t n, int S, int64_t T) {
   WsLayout w{0, 0, 0, 0};
   const int64_t C = (S == 0 || T <= 0) ? 1 : ceil_div(n, T);
-  if (C <= 1 || fused_ok(S, C)) return w;
+  if (C <= 1 || fused_ok(S, C, T)) return w;
   const size_t D = 2 * (size_t)S;
   w.p_off = 0;
   w.e_off = align256(D * D * sizeof(double));
@@ -546,40 +605,32 @@ int padded_stages(int S) {
 template <int S>
 int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
               const SosParams& p, int clip, int64_t T, const double* G, int p1mode, int vec_x,
-              int vec_y, hipStream_t s) {
+              int vec_y, const XState& XS, hipStream_t s) {
   static_assert(2 * S <= 16, "scan matrix is at most 16 x 16");
   ScanParams sp;
   const std::vector<double> P = chunk_transition(p, S, T);
   for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
   const int C = (int)ceil_div(n, T);
-  // 64 chunk lanes per channel (4 channels per block) when the row splits into
-  // <= 64 chunks, else 256 (one channel per block).
-  const int CB = (C <= 64) ? 64 : 256;
-  const int CHN = kNT / CB;
-  const dim3 grid((unsigned)ceil_div(B, CHN));
-  TraceScope trace(p1mode == 2 ? "iir_apply" : "iir_fused", s);
+  TraceScope trace(p1mode == 2 ? "iir_xstate" : "iir_fused", s);
   // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
   // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
-  // need every block's output span to fit a 31-bit byte offset.
-  const bool span_ok = (int64_t)CHN * ld_y * 4 < (int64_t)kOob;
+  // address one channel's row with a 31-bit byte offset.
+  const bool span_ok = n * 4 < (int64_t)kOob;
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
-#define DSP_FUSED_LAUNCH(P1v, VMv, CBv)                                                        \
-  hipLaunchKernelGGL((k_iir_fused<S, P1v, VMv, CBv>), grid, dim3(kNT), 0, s, x, y, B, n, ld_x, \
-                     ld_y, p, sp, G, T, C, clip, vec_x, vec_y)
-#define DSP_FUSED_CB(P1v, VMv)                   \
-  if (CB == 64) DSP_FUSED_LAUNCH(P1v, VMv, 64);  \
-  else DSP_FUSED_LAUNCH(P1v, VMv, 256);
-#define DSP_FUSED_VM(P1v)                        \
-  if (VMr == 1) { DSP_FUSED_CB(P1v, 1) }         \
-  else if (VMr == 2) { DSP_FUSED_CB(P1v, 2) }    \
-  else { DSP_FUSED_CB(P1v, 0) }
-  if (p1mode == 2) { DSP_FUSED_VM(2) }
-  else if (p1mode == 1) { DSP_FUSED_VM(1) }
-  else { DSP_FUSED_VM(0) }
-#undef DSP_FUSED_VM
-#undef DSP_FUSED_CB
-#undef DSP_FUSED_LAUNCH
-  DSP_LAUNCHED("k_iir_fused");
+  const dim3 grid((unsigned)B);
+#define DSP_WAVE_LAUNCH(P1v, VMv)                                                            \
+  hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv>), grid, dim3(kWave), 0, s, x, y, B, n, ld_x,   \
+                     ld_y, p, sp, G, T, C, clip, XS)
+#define DSP_WAVE_VM(P1v)                         \
+  if (VMr == 1) DSP_WAVE_LAUNCH(P1v, 1);         \
+  else if (VMr == 2) DSP_WAVE_LAUNCH(P1v, 2);    \
+  else DSP_WAVE_LAUNCH(P1v, 0);
+  if (p1mode == 2) { DSP_WAVE_VM(2) }
+  else if (p1mode == 1) { DSP_WAVE_VM(1) }
+  else { DSP_WAVE_VM(0) }
+#undef DSP_WAVE_VM
+#undef DSP_WAVE_LAUNCH
+  DSP_LAUNCHED("k_iir_wave");
   return DSP_OK;
 }
 
@@ -634,38 +685,63 @@ int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
   const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
   const int64_t C = (S == 0) ? 1 : ceil_div(n, T);
   if constexpr (S >= 1 && S <= 8 && S != 7) {
-    if (fused_ok(S, C))
-      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, G ? 1 : 0, vec_x, vec_y, s);
+    if (fused_ok(S, C, T))
+      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, G ? 1 : 0, vec_x, vec_y,
+                          XState{}, s);
   }
   return run_general<S>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
 }
 
 }  // namespace
 
-int fused_cascade_ok(int S, int64_t n, int64_t chunk_len) {
-  return S == padded_stages(S) && chunk_len > 0 && chunk_len % kTS == 0 &&
-         fused_ok(S, ceil_div(n, chunk_len));
+int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
+                    int64_t* q0, int64_t* rows) {
+  DSP_REQUIRE(chunk_len > 0 && K >= 1 && L >= 1 && M >= 1 && c >= 0, "bad SRC/chunk geometry");
+  DSP_REQUIRE((chunk_len * M) % L == 0, "chunk_len*M=%lld is not a multiple of L=%d",
+              (long long)(chunk_len * M), L);
+  const int64_t sh = chunk_len * M / L;
+  DSP_REQUIRE(sh % 4 == 0, "chunk input shift %lld is not a multiple of 4", (long long)sh);
+  // q' of output t = 0..T-1 and tap k = 0..K-1: (t*M + c - k) / L where divisible.
+  auto floor_div = [](int64_t a, int64_t d) { return a >= 0 ? a / d : -((-a + d - 1) / d); };
+  const int64_t qmax = floor_div((chunk_len - 1) * M + c, L);
+  const int64_t qmin = -floor_div(K - 1 - c, L);  // ceil((c - K + 1) / L)
+  const int64_t lo = floor_div(qmin, 4) * 4;
+  const int64_t span = qmax - lo + 1;
+  *shift = sh;
+  *q0 = lo;
+  *rows = ceil_div(span, kTS) * kTS;
+  return DSP_OK;
 }
 
-int launch_biquad_from_states(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
-                              int64_t ld_y, const double* sos, int S, int clip,
-                              int64_t chunk_len, const double* E, hipStream_t s) {
-  DSP_REQUIRE(fused_cascade_ok(S, n, chunk_len), "no fused cascade for S=%d n=%lld T=%lld", S,
-              (long long)n, (long long)chunk_len);
-  DSP_REQUIRE(x && y && sos && E, "null pointer");
+int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                         int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
+                         const float* xs, int64_t n_in, int64_t ld_xs, int K, int L, int M,
+                         int64_t c, const double* gx, int64_t gx_rows, hipStream_t s) {
+  DSP_REQUIRE(S >= 1 && S <= 8 && S != 7, "x-domain states need 1 <= S <= 8, S != 7 (S=%d)", S);
+  DSP_REQUIRE(fused_ok(S, ceil_div(n, chunk_len), chunk_len),
+              "x-domain states need the fused cascade (n=%lld chunk_len=%lld)", (long long)n,
+              (long long)chunk_len);
+  XState XS{xs, ld_xs, n_in, 0, 0, 0};
+  if (int rc = xstate_geometry(chunk_len, K, L, M, c, &XS.shift, &XS.q0, &XS.rows)) return rc;
+  DSP_REQUIRE(gx_rows == XS.rows, "x-domain state table has %lld rows, geometry needs %lld",
+              (long long)gx_rows, (long long)XS.rows);
+  DSP_REQUIRE(x && y && sos && xs && gx, "null pointer");
+  DSP_REQUIRE((ld_xs & 3) == 0 && (reinterpret_cast<uintptr_t>(xs) & 15) == 0 && ld_xs >= n_in,
+              "x-domain states need 16-byte aligned SRC input rows");
   SosParams p;
   for (int k = 0; k < DSP_MAX_STAGES; ++k)
     for (int i = 0; i < 5; ++i) p.c[k][i] = (k < S) ? sos[5 * k + i] : (i == 0 ? 1.0 : 0.0);
   const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
   const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
+  const int64_t T = chunk_len;
   switch (S) {
-    case 1: return run_fused<1>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 2: return run_fused<2>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 3: return run_fused<3>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 4: return run_fused<4>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 5: return run_fused<5>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 6: return run_fused<6>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
-    case 8: return run_fused<8>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, E, 2, vec_x, vec_y, s);
+    case 1: return run_fused<1>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 2: return run_fused<2>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 3: return run_fused<3>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 4: return run_fused<4>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 5: return run_fused<5>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 6: return run_fused<6>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 8: return run_fused<8>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
 }

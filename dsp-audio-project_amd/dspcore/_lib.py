@@ -19,7 +19,8 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libdspcore.so")
+# DSPCORE_LIB: alternate build of the same ABI (tuning experiments only).
+LIB_PATH = os.environ.get("DSPCORE_LIB") or os.path.join(PKG_ROOT, "lib", "libdspcore.so")
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "dspcore.h")
 
 DSP_OK = 0
@@ -50,9 +51,12 @@ _SIGNATURES = {
         _vp]),
     "dsp_chain_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
-        _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _c_i64,
-        _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+        _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,
+        _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i64]),
+    "dsp_chain_xstate_geometry": (ctypes.c_int, [
+        _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64),
+        ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "dsp_trace_enable": (ctypes.c_int, [_c_i32]),
     "dsp_trace_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _c_i32]),
 }

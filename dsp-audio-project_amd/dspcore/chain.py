@@ -13,7 +13,7 @@ import torch
 
 from . import _lib, ops
 from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, spectrum_plan,
-                     src_plan)
+                     src_plan, xstate_chunk_len)
 
 
 @dataclass(frozen=True)
@@ -32,7 +32,8 @@ class Chain:
     """Device-resident plan of the chain for a fixed batch size."""
 
     def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
-                 chunk_len: int | None = None, use_table: bool = True):
+                 chunk_len: int | None = None, use_table: bool = True,
+                 use_xstate: bool = True):
         ops.require_gpu()
         self.cfg = cfg
         self.B = int(batch)
@@ -47,7 +48,19 @@ class Chain:
         self.eq: EqPlan = eq_plan(self.fs_out, cfg.gains)
         spec_len = n_out if cfg.limit_pts is None else min(n_out, cfg.limit_pts)
         self.spec: SpectrumPlan = spectrum_plan(spec_len, cfg.n_fft)
-        self.chunk_len = chunk_len_for(n_out) if chunk_len is None else int(chunk_len)
+        S = self.eq.sos.shape[0]
+        # x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
+        # length with chunk_len*M/L a multiple of 4; take it unless it would cut
+        # the row into far fewer chunks than the plain rule.
+        plain = chunk_len_for(n_out)
+        xs_len = xstate_chunk_len(n_out, cfg.L, cfg.M)
+        self.xstate = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
+                       and 1 <= S <= 8 and S != 7 and xs_len <= 2 * plain
+                       and (chunk_len is None or int(chunk_len) == xs_len))
+        if chunk_len is not None:
+            self.chunk_len = int(chunk_len)
+        else:
+            self.chunk_len = xs_len if self.xstate else plain
         dev = self.device
         self.taps = ops.taps_tensor(self.src, dev)
         self.window = ops._table("hann", self.spec.n_fft, dev)
@@ -61,6 +74,8 @@ class Chain:
                                                          self.chunk_len)
         self.workspace = torch.empty(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
         self.table = ops.state_table(self.sos, self.chunk_len, dev) if use_table else None
+        self.xtable, self.xrows = (ops.xstate_table(self.sos, self.src, self.chunk_len, dev)
+                                   if self.xstate else (None, 0))
 
     # -- algorithmic traffic ---------------------------------
     def algorithmic_bytes(self) -> int:
@@ -92,8 +107,8 @@ class Chain:
                 x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.mag.data_ptr(),
                 self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.y),
                 self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
-                sos_ptr, S, clip, self.chunk_len, ops._ptr(self.table), self.spec.seg_start,
-                self.spec.seg_len,
+                sos_ptr, S, clip, self.chunk_len, ops._ptr(self.table), ops._ptr(self.xtable),
+                self.xrows, self.spec.seg_start, self.spec.seg_len,
                 self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)
@@ -102,7 +117,9 @@ class Chain:
 
     def run_stages(self, x: torch.Tensor, events: list | None = None):
         """Same pass, one entry point per stage; optional (start, end) event pairs
-        around each stage for per-kernel timing on the current stream."""
+        around each stage for per-kernel timing on the current stream.  y is
+        bitwise that of run(); z may differ from run()'s by rounding when run()
+        takes its chunk states from x (both within the EQ tolerance)."""
         x = self.check_input(x)
 
         def mark(i, which):

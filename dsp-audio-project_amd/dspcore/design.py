@@ -8,6 +8,7 @@ taps, fp64 second-order sections, sizes) cross into the HIP kernels.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 
 import numpy as np
@@ -200,6 +201,45 @@ def state_response_table(sos: np.ndarray, chunk_len: int) -> np.ndarray:
         m += k
         Am = Am @ Am
     return np.ascontiguousarray(G[::-1])
+
+
+def xstate_chunk_len(n_out: int, L: int, M: int, max_chunks: int = 64) -> int:
+    """Chunk length for the chain's x-domain chunk states (include/dspcore.h,
+    dsp_chain_f32): the smallest multiple of 32 with chunk_len*M/L an integer
+    multiple of 4 that splits n_out into <= max_chunks chunks.  A function of
+    (n_out, L, M) only, so rows stay independent of the batch size."""
+    unit = 4 * L // math.gcd(M, 4 * L)          # chunk_len*M % (4L) == 0
+    step = 32 * unit // math.gcd(32, unit)      # lcm(32, unit)
+    per = -(-int(n_out) // max_chunks)
+    return max(step, -(-per // step) * step)
+
+
+def xstate_table(sos: np.ndarray, plan: "SrcPlan", chunk_len: int, q0: int,
+                 rows: int) -> np.ndarray:
+    """float64 [rows][2S]: the state-response table of `chunk_len` composed with
+    the SRC taps, so that a chunk's zero-state end state is a dot product over
+    the SRC input instead of its output (include/dspcore.h, dsp_chain_f32):
+
+        E_c = sum_t G[t] y[cT + t],  y[m] = sum_k (L h)[k] x[(m M + c - k) / L]
+            = sum_j Gx[j] x[c T M / L + q0 + j],
+        Gx[q' - q0] = sum_t G[t] (L h)[t M + c - q' L]   (0 <= t M + c - q' L < K).
+
+    Everything in float64 from the reference's own taps (dsp_core.py:159-162)."""
+    G = state_response_table(sos, chunk_len)
+    T, D = G.shape
+    L, M, K, c = plan.L, plan.M, plan.K, plan.c_offset
+    taps = np.asarray(plan.taps, dtype=np.float64)
+    base = np.arange(T, dtype=np.int64) * M + c
+    ph, qb = base % L, base // L
+    out = np.zeros((rows, D))
+    for j in range(-(-K // L) + 1):
+        k = ph + j * L
+        ok = k < K
+        q = qb[ok] - j - q0
+        if q.size and (q.min() < 0 or q.max() >= rows):
+            raise ValueError("x-state geometry does not cover the taps")
+        np.add.at(out, q, G[ok] * taps[k[ok], None])
+    return np.ascontiguousarray(out)
 
 
 @dataclass(frozen=True)

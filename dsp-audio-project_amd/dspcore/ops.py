@@ -15,6 +15,7 @@ import torch
 
 from . import _lib
 from .design import SrcPlan, chunk_len_for, hann, state_response_table, twiddles
+from .design import xstate_table as xstate_table_host
 
 _tables_lock = threading.Lock()
 _tables: dict = {}
@@ -119,6 +120,36 @@ def state_table(sos: np.ndarray, chunk_len: int, device: torch.device) -> torch.
                 t = torch.from_numpy(state_response_table(sos, chunk_len)).to(device)
                 _tables[key] = t
     return t
+
+
+def xstate_geometry(chunk_len: int, plan: SrcPlan) -> tuple[int, int, int]:
+    """(shift, q0, rows) of the chain's x-domain chunk states, from the library
+    (dsp_chain_xstate_geometry) so host table and kernel agree by construction."""
+    import ctypes
+    sh, q0, rows = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = _lib.load().dsp_chain_xstate_geometry(int(chunk_len), plan.K, plan.L, plan.M,
+                                               plan.c_offset, ctypes.byref(sh),
+                                               ctypes.byref(q0), ctypes.byref(rows))
+    _lib.check(rc, "dsp_chain_xstate_geometry")
+    return sh.value, q0.value, rows.value
+
+
+def xstate_table(sos: np.ndarray, plan: SrcPlan, chunk_len: int,
+                 device: torch.device) -> tuple[torch.Tensor, int]:
+    """Cached device copy of design.xstate_table and its row count."""
+    _, q0, rows = xstate_geometry(chunk_len, plan)
+    key = ("GX", sos.tobytes(), plan.L, plan.M, plan.K, plan.c_offset, chunk_len, device.index)
+    t = _tables.get(key)
+    if t is None:
+        with _tables_lock:
+            t = _tables.get(key)
+            if t is None:
+                if len(_tables) > 256:
+                    for k in [k for k in _tables if k[0] in ("G", "GX")]:
+                        del _tables[k]
+                t = torch.from_numpy(xstate_table_host(sos, plan, chunk_len, q0, rows)).to(device)
+                _tables[key] = t
+    return t, rows
 
 
 def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,

@@ -118,14 +118,31 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
  * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes().
  * Each row's result is bitwise independent of B.
+ *
+ * Chunk end states of the cascade.  With `xstate_table` (device, float64
+ * [xstate_rows][2S], may be NULL) the cascade's first pass reads x instead of
+ * y: chunk c's zero-state end state is
+ *     E_c = sum_j xstate_table[j] * x[c*shift + q0 + j],   j < xstate_rows
+ * (x == 0 outside [0, n_in)), where (shift, q0, xstate_rows) come from
+ * dsp_chain_xstate_geometry and row j = sum_t G[t] (L h)[t*M + c_offset -
+ * (q0 + j)*L] composes the state-response table G of chunk_len (see
+ * dsp_biquad_cascade_f32) with the float64 taps.  It needs 1 <= S <= 8,
+ * S != 7, ceil(n_out / chunk_len) <= 64, chunk_len a multiple of 32,
+ * chunk_len*M/L an integer multiple of 4 and 16-byte aligned rows of x.
+ * Otherwise `state_table` (G, may be NULL) is used as in
+ * dsp_biquad_cascade_f32.
  * ------------------------------------------------------------------------- */
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S,
                                  int64_t chunk_len);
+int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
+                              int64_t c_offset, int64_t* shift, int64_t* q0,
+                              int64_t* rows);
 int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t n_in, int64_t ld_x, int64_t n_out, int64_t ld_y,
                   const float* taps, int32_t K, int32_t L, int32_t M,
                   int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
+                  const double* xstate_table, int64_t xstate_rows,
                   int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
                   size_t workspace_bytes, void* stream);

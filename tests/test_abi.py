@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 11
+    assert len(names) == 12
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 10000
+    assert lib.dsp_version() == 10100
     assert isinstance(_lib.last_error(), str)
 
 
@@ -64,3 +64,19 @@ def test_trace_toggle_without_gpu():
     assert _lib.load().dsp_trace_enable(1) == 0
     assert _lib.trace_read() == []          # nothing launched
     assert _lib.load().dsp_trace_enable(0) == 0
+
+
+def test_xstate_geometry_query():
+    """dsp_chain_xstate_geometry is host-only: shift = T*M/L, q0 a multiple of 4
+    at or below the lowest input index a chunk's outputs touch, rows a multiple
+    of 32 covering the highest."""
+    lib = _lib.load()
+    out = [ctypes.c_int64() for _ in range(3)]
+    refs = [ctypes.byref(o) for o in out]
+    assert lib.dsp_chain_xstate_geometry(1152, 121, 3, 2, 60, *refs) == 0
+    shift, q0, rows = (o.value for o in out)
+    assert shift == 768 and q0 % 4 == 0 and rows % 32 == 0
+    assert q0 <= -((121 - 1 - 60) // 3) and q0 + rows > (1151 * 2 + 60) // 3
+    # chunk_len*M not a multiple of L, or a shift that is not a multiple of 4
+    assert lib.dsp_chain_xstate_geometry(1000, 121, 3, 2, 60, *refs) == _lib.DSP_EINVAL
+    assert lib.dsp_chain_xstate_geometry(1149, 121, 3, 2, 60, *refs) == _lib.DSP_EINVAL

@@ -250,11 +250,19 @@ def test_chain_matches_reference(gpu, tag, fs, L, M, K):
     assert np.max(np.abs(z - g[f"{tag}_z"])) <= EQ_ATOL
     ref = g[f"{tag}_mag"]
     assert np.max(np.abs(mag - ref)) <= CHAIN_MAG_RTOL * np.max(ref)
-    # the staged path (one ABI call per stage) gives the same bits
+    # the staged path (one ABI call per stage): y bitwise; z within rounding of
+    # the fused chain, whose chunk states come from x through the composed
+    # table instead of from y (same float64 states up to ~1e-15 relative)
     y2, z2, m2 = (t.cpu().numpy()[0] for t in ch.run_stages(x))
     np.testing.assert_array_equal(y2, y)
-    np.testing.assert_array_equal(z2, z)
-    np.testing.assert_array_equal(m2, mag)
+    assert np.max(np.abs(z2 - z)) <= 2e-6
+    assert np.max(np.abs(m2 - mag)) <= 1e-5 * np.max(mag)
+    if ch.xstate:
+        # and without x-domain states the fused call gives the staged bits
+        ch2 = Chain(cfg, 1, gpu, use_xstate=False, chunk_len=ch.chunk_len)
+        y3, z3, m3 = (t.cpu().numpy()[0] for t in ch2.run(x))
+        np.testing.assert_array_equal(z3, z2)
+        np.testing.assert_array_equal(m3, m2)
 
 
 def test_chain_config3_full_batch(gpu):

@@ -120,3 +120,37 @@ def test_chunk_policy_is_batch_independent_and_fused():
         assert T % 32 == 0 and T >= 32
         assert -(-n // T) <= 64
     assert design.chunk_len_for(72000) == 1152
+
+
+def test_xstate_table_reproduces_output_domain_states():
+    """The chain's x-domain state table (design.xstate_table) gives the same
+    chunk end states as the output-domain table applied to the float64 SRC
+    output of the reference's own algorithm (np.convolve 'same', [::M])."""
+    import ctypes
+
+    from dspcore import _lib, design
+    lib = _lib.load()
+    gains = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3,
+             "Presence": 5, "Brilliance": -6}
+    for n_in, fs, L, M, K in [(4800, 48000, 3, 2, None), (4801, 48000, 3, 2, 255),
+                              (9600, 44100, 160, 147, 1023), (3000, 48000, 2, 1, None)]:
+        plan = design.src_plan(n_in, fs, M, L, K)
+        sos = design.eq_plan(plan.fs_out, gains).sos
+        T = design.xstate_chunk_len(plan.n_out, L, M)
+        assert T % 32 == 0 and (T * M) % (4 * L) == 0 and -(-plan.n_out // T) <= 64
+        out = [ctypes.c_int64() for _ in range(3)]
+        assert lib.dsp_chain_xstate_geometry(T, plan.K, L, M, plan.c_offset,
+                                             *[ctypes.byref(o) for o in out]) == 0
+        shift, q0, rows = (o.value for o in out)
+        gx = design.xstate_table(sos, plan, T, q0, rows)
+        g = design.state_response_table(sos, T)
+        x = np.random.default_rng(n_in).uniform(-1, 1, n_in)
+        xe = np.zeros(n_in * L)
+        xe[::L] = x
+        y = np.convolve(xe, plan.taps, "same")[::M]
+        for c in range(-(-plan.n_out // T) - 1):
+            e_y = g.T @ y[c * T:(c + 1) * T]
+            idx = c * shift + q0 + np.arange(rows)
+            xv = np.where((idx >= 0) & (idx < n_in), x[np.clip(idx, 0, n_in - 1)], 0.0)
+            e_x = gx.T @ xv
+            assert np.max(np.abs(e_x - e_y)) <= 1e-12 * max(1.0, np.max(np.abs(e_y)))
