@@ -3,8 +3,16 @@
 // Replaces reference modules/dsp_core.py:233-254: the serial loop of
 // aplicar_ecuacion_diferencias (= scipy.signal.lfilter(b, a, x), :205-214) over
 // the EQ bands followed by np.clip(y, -1, 1) (:254).  lfilter realises each
-// biquad in direct form II transposed with zero initial state:
-//     v = b0 u + s1;  s1 = b1 u - a1 v + s2;  s2 = b2 u - a2 v
+// biquad in direct form II transposed with zero initial state.  The kernels
+// realise the same transfer functions in direct form II with the b0 gains
+// pulled out (every b0 != 0, as for every EQ band):
+//     u *= G = prod b0;  per stage:  w = u - a1 w1 - a2 w2
+//                                    v = w + (b1/b0) w1 + (b2/b0) w2
+// i.e. 4 fp64 FMAs per stage instead of DF2T's 4 FMAs + 1 multiply (25 vs 30
+// per sample for the 6-band EQ); with some b0 == 0 the stage keeps its gain
+// (v = b0 w + b1 w1 + b2 w2, NORM = false).  Both are exact rearrangements of
+// the same recursion; in float64 they differ from lfilter's DF2T by rounding
+// only (~1e-12 here against the 1e-5 tolerance).
 // Float64 state and coefficients are mandatory: the 40 Hz band has poles at
 // |r| = 0.99926 and a float32 recursion drifts by ~1e-3.
 //
@@ -43,9 +51,43 @@
 namespace dsp {
 namespace {
 
+// Direct form II realisation: c[k] = {g, c1, c2, a1, a2} and input gain G.
+// NORM (every b0 != 0): g = 1, c1 = b1/b0, c2 = b2/b0, G = prod b0.
+// Otherwise: g = b0, c1 = b1, c2 = b2, G = 1.  Stages past S are identities.
 struct SosParams {
-  double c[DSP_MAX_STAGES][5];  // b0 b1 b2 a1 a2
+  double c[DSP_MAX_STAGES][5];
+  double G;
 };
+
+// Host: realisation of a [S][5] {b0 b1 b2 a1 a2} cascade; returns NORM.  Must
+// match dspcore/design.py:df2_realization, which builds the state tables.
+bool realize(const double* sos, int S, SosParams* p) {
+  bool norm = true;
+  for (int k = 0; k < S; ++k) norm = norm && sos[5 * k] != 0.0;
+  p->G = 1.0;
+  for (int k = 0; k < DSP_MAX_STAGES; ++k) {
+    double* c = p->c[k];
+    if (k >= S) {
+      c[0] = 1.0;
+      c[1] = c[2] = c[3] = c[4] = 0.0;
+      continue;
+    }
+    const double* r = sos + 5 * k;
+    if (norm) {
+      c[0] = 1.0;
+      c[1] = r[1] / r[0];
+      c[2] = r[2] / r[0];
+      p->G *= r[0];
+    } else {
+      c[0] = r[0];
+      c[1] = r[1];
+      c[2] = r[2];
+    }
+    c[3] = r[3];
+    c[4] = r[4];
+  }
+  return norm;
+}
 struct ScanParams {
   double P[16 * 16];  // A^T, row-major D x D, D = 2S <= 16
 };
@@ -59,23 +101,28 @@ constexpr int kCBMax = kWave;  // max chunks per channel in the fused kernel
 #define DSP_IIR_EXPERIMENT 0  // 1: no arithmetic, 2: no global loads (timing only)
 #endif
 
-template <int S>
-__device__ __forceinline__ double cascade_step(double u, double (&s1)[S > 0 ? S : 1],
-                                               double (&s2)[S > 0 ? S : 1],
+// One sample through the S-stage cascade; w1/w2 are the stages' delay lines.
+template <int S, bool NORM>
+__device__ __forceinline__ double cascade_step(double u, double (&w1)[S > 0 ? S : 1],
+                                               double (&w2)[S > 0 ? S : 1],
                                                const SosParams& p) {
+  if constexpr (NORM && S > 0) u *= p.G;
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    const double v = fma(p.c[k][0], u, s1[k]);
-    s1[k] = fma(-p.c[k][3], v, fma(p.c[k][1], u, s2[k]));
-    s2[k] = fma(-p.c[k][4], v, p.c[k][2] * u);
-    u = v;
+    const double w = fma(-p.c[k][4], w2[k], fma(-p.c[k][3], w1[k], u));
+    const double h = NORM ? w : p.c[k][0] * w;
+    u = fma(p.c[k][2], w2[k], fma(p.c[k][1], w1[k], h));
+    w2[k] = w1[k];
+    w1[k] = w;
   }
   return u;
 }
 
-__device__ __forceinline__ double clip1(double v) {
-  // np.clip semantics: NaN stays NaN.
-  return v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+__device__ __forceinline__ float clip1(float v) {
+  // np.clip semantics: NaN stays NaN.  Clipping after the float32 rounding
+  // gives the same result as rounding the float64 clip (|v| <= 1 rounds to
+  // |v| <= 1, and anything beyond rounds to beyond-or-equal).
+  return v < -1.f ? -1.f : (v > 1.f ? 1.f : v);
 }
 
 // Row descriptors live in LDS: global offset of the row's first sample for
@@ -206,7 +253,7 @@ enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
 // tile's loads in flight during the current tile's arithmetic.  Samples outside
 // a row's range are zeros; their outputs are never stored.  Starts with a
 // hand-off (fetch reads other threads' row descriptors) and ends with one.
-template <int S, int MODE, int NR, int VM, bool VIN>
+template <int S, int MODE, int NR, int VM, bool VIN, bool NORM>
 __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __restrict__ y,
                                          __amdgpu_buffer_rsrc_t rsrc, float* tile,
                                          const Rows& rows, int64_t T, int tid,
@@ -249,8 +296,8 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
     } else {
 #pragma unroll 8
       for (int j = 0; j < kTS; ++j) {
-        const double out = cascade_step<S>((double)my[j], s1, s2, p);
-        if constexpr (MODE == kApply) my[j] = (float)(clip ? clip1(out) : out);
+        const float out = (float)cascade_step<S, NORM>((double)my[j], s1, s2, p);
+        if constexpr (MODE == kApply) my[j] = clip ? clip1(out) : out;
       }
     }
     if constexpr (MODE == kApply) {
@@ -284,7 +331,7 @@ struct XState {
 // Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
 constexpr int kWaveTileFloats = kWave * kRow;
 
-template <int S, int P1, int VM>
+template <int S, int P1, int VM, bool NORM>
 __global__ __launch_bounds__(kWave) void k_iir_wave(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
     int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
@@ -328,13 +375,13 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   if constexpr (P1 == 2) {
-    run_pass<S, kStateTable, kWave, VM, true>(XS.xs, y, rsrc, tile, rows, XS.rows, c, s1, s2,
+    run_pass<S, kStateTable, kWave, VM, true, NORM>(XS.xs, y, rsrc, tile, rows, XS.rows, c, s1, s2,
                                                e, p, G, clip);
   } else if constexpr (P1 == 1) {
-    run_pass<S, kStateTable, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p,
+    run_pass<S, kStateTable, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p,
                                                    G, clip);
   } else {
-    run_pass<S, kStateCascade, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e,
+    run_pass<S, kStateCascade, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e,
                                                      p, G, clip);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -384,14 +431,14 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
   asm volatile("" ::: "memory");
 
   // ---- pass 2: outputs from the carried state
-  run_pass<S, kApply, kWave, VM, (VM > 0)>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p, G,
+  run_pass<S, kApply, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p, G,
                                             clip);
 }
 
 // ---------------------------------------------------------------------------
 // General path (C > kCB or S > 8): separate pass / carry launches.
 // ---------------------------------------------------------------------------
-template <int S, bool APPLY>
+template <int S, bool APPLY, bool NORM>
 __global__ __launch_bounds__(kNT) void k_iir_pass(
     const float* __restrict__ x, float* __restrict__ y, int64_t n, int64_t ld_x,
     int64_t ld_y, SosParams p, int64_t C, int64_t T, int64_t lanes,
@@ -431,10 +478,10 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
   // Rows span many channels here: guarded loads and stores (VM 0).
   const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0, 0x00020000);
   if (vec_x)
-    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, true>(x, y, none, tile, rows, T, tid, s1,
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, true, NORM>(x, y, none, tile, rows, T, tid, s1,
                                                               s2, e, p, nullptr, clip);
   else
-    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, false>(x, y, none, tile, rows, T, tid,
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, false, NORM>(x, y, none, tile, rows, T, tid,
                                                                s1, s2, e, p, nullptr, clip);
   if (!APPLY && live) {
     double* eo = e_out + g * (2 * S);
@@ -478,6 +525,19 @@ __global__ __launch_bounds__(256) void k_iir_carry(const double* __restrict__ P,
   }
 }
 
+// One step of the realisation's state (w1_0, w2_0, w1_1, ...) with zero input:
+// the columns of A.  Host and device (general path) share it.
+__host__ __device__ inline void zero_input_step(const SosParams& p, int S, double* X) {
+  double u = 0.0;
+  for (int k = 0; k < S; ++k) {
+    const double w = u - p.c[k][3] * X[2 * k] - p.c[k][4] * X[2 * k + 1];
+    const double v = p.c[k][0] * w + p.c[k][1] * X[2 * k] + p.c[k][2] * X[2 * k + 1];
+    X[2 * k + 1] = X[2 * k];
+    X[2 * k] = w;
+    u = v;
+  }
+}
+
 // Builds A (one cascade step on each unit state, zero input) and P = A^T by
 // square-and-multiply in float64 inside one workgroup (general path; the fused
 // path gets A^T from the host as a kernel argument).
@@ -489,15 +549,7 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
   if (tid < D) {
     double X[32];
     for (int i = 0; i < D; ++i) X[i] = (i == tid) ? 1.0 : 0.0;
-    double u = 0.0;
-    for (int k = 0; k < S; ++k) {
-      const double v = p.c[k][0] * u + X[2 * k];
-      const double n1 = p.c[k][1] * u - p.c[k][3] * v + X[2 * k + 1];
-      const double n2 = p.c[k][2] * u - p.c[k][4] * v;
-      X[2 * k] = n1;
-      X[2 * k + 1] = n2;
-      u = v;
-    }
+    zero_input_step(p, S, X);
     for (int i = 0; i < D; ++i) sA[i * D + tid] = X[i];
   }
   const int r = tid / 32, c = tid % 32;
@@ -529,22 +581,14 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-// A of the D = 2S state system (state order s1_0, s2_0, s1_1, ...), float64.
+// A of the D = 2S state system (state order w1_0, w2_0, w1_1, ...), float64.
 std::vector<double> state_matrix(const SosParams& p, int S) {
   const int D = 2 * S;
   std::vector<double> A((size_t)D * D, 0.0);
   for (int col = 0; col < D; ++col) {
     std::vector<double> X(D, 0.0);
     X[col] = 1.0;
-    double u = 0.0;
-    for (int k = 0; k < S; ++k) {
-      const double v = p.c[k][0] * u + X[2 * k];
-      const double n1 = p.c[k][1] * u - p.c[k][3] * v + X[2 * k + 1];
-      const double n2 = p.c[k][2] * u - p.c[k][4] * v;
-      X[2 * k] = n1;
-      X[2 * k + 1] = n2;
-      u = v;
-    }
+    zero_input_step(p, S, X.data());
     for (int r = 0; r < D; ++r) A[(size_t)r * D + col] = X[r];
   }
   return A;
@@ -604,8 +648,8 @@ int padded_stages(int S) {
 
 template <int S>
 int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
-              const SosParams& p, int clip, int64_t T, const double* G, int p1mode, int vec_x,
-              int vec_y, const XState& XS, hipStream_t s) {
+              const SosParams& p, bool norm, int clip, int64_t T, const double* G, int p1mode,
+              int vec_x, int vec_y, const XState& XS, hipStream_t s) {
   static_assert(2 * S <= 16, "scan matrix is at most 16 x 16");
   ScanParams sp;
   const std::vector<double> P = chunk_transition(p, S, T);
@@ -618,23 +662,26 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const bool span_ok = n * 4 < (int64_t)kOob;
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
   const dim3 grid((unsigned)B);
-#define DSP_WAVE_LAUNCH(P1v, VMv)                                                            \
-  hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv>), grid, dim3(kWave), 0, s, x, y, B, n, ld_x,   \
-                     ld_y, p, sp, G, T, C, clip, XS)
-#define DSP_WAVE_VM(P1v)                         \
-  if (VMr == 1) DSP_WAVE_LAUNCH(P1v, 1);         \
-  else if (VMr == 2) DSP_WAVE_LAUNCH(P1v, 2);    \
-  else DSP_WAVE_LAUNCH(P1v, 0);
-  if (p1mode == 2) { DSP_WAVE_VM(2) }
-  else if (p1mode == 1) { DSP_WAVE_VM(1) }
-  else { DSP_WAVE_VM(0) }
+#define DSP_WAVE_LAUNCH(P1v, VMv, NV)                                                       \
+  hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV>), grid, dim3(kWave), 0, s, x, y, B, n,     \
+                     ld_x, ld_y, p, sp, G, T, C, clip, XS)
+#define DSP_WAVE_VM(P1v, NV)                         \
+  if (VMr == 1) DSP_WAVE_LAUNCH(P1v, 1, NV);         \
+  else if (VMr == 2) DSP_WAVE_LAUNCH(P1v, 2, NV);    \
+  else DSP_WAVE_LAUNCH(P1v, 0, NV);
+  // The state tables are built for the NORM realisation (the EQ's); a cascade
+  // with some b0 == 0 runs pass 1 as the cascade itself.
+  if (!norm) { DSP_WAVE_VM(0, false) }
+  else if (p1mode == 2) { DSP_WAVE_VM(2, true) }
+  else if (p1mode == 1) { DSP_WAVE_VM(1, true) }
+  else { DSP_WAVE_VM(0, true) }
 #undef DSP_WAVE_VM
 #undef DSP_WAVE_LAUNCH
   DSP_LAUNCHED("k_iir_wave");
   return DSP_OK;
 }
 
-template <int S>
+template <int S, bool NORM>
 int run_general(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
                 const SosParams& p, int clip, int64_t T, void* ws, int vec_x, int vec_y,
                 hipStream_t s) {
@@ -654,7 +701,7 @@ int run_general(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
     const int64_t lanes1 = B * (C - 1);
     {
       TraceScope trace("iir_state", s);
-      hipLaunchKernelGGL((k_iir_pass<S, false>), dim3((unsigned)ceil_div(lanes1, kNT)),
+      hipLaunchKernelGGL((k_iir_pass<S, false, NORM>), dim3((unsigned)ceil_div(lanes1, kNT)),
                          dim3(kNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes1,
                          (const double*)nullptr, E, clip, vec_x, vec_y);
     }
@@ -669,7 +716,7 @@ int run_general(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
   const int64_t lanes2 = B * C;
   {
     TraceScope trace("iir_apply", s);
-    hipLaunchKernelGGL((k_iir_pass<S, true>), dim3((unsigned)ceil_div(lanes2, kNT)),
+    hipLaunchKernelGGL((k_iir_pass<S, true, NORM>), dim3((unsigned)ceil_div(lanes2, kNT)),
                        dim3(kNT), 0, s, x, y, n, ld_x, ld_y, p, C, T, lanes2, SI,
                        (double*)nullptr, clip, vec_x, vec_y);
   }
@@ -679,17 +726,18 @@ int run_general(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
 
 template <int S>
 int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
-                const SosParams& p, int clip, int64_t T, const double* G, void* ws,
+                const SosParams& p, bool norm, int clip, int64_t T, const double* G, void* ws,
                 hipStream_t s) {
   const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
   const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
   const int64_t C = (S == 0) ? 1 : ceil_div(n, T);
   if constexpr (S >= 1 && S <= 8 && S != 7) {
     if (fused_ok(S, C, T))
-      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, clip, T, G, G ? 1 : 0, vec_x, vec_y,
+      return run_fused<S>(x, y, B, n, ld_x, ld_y, p, norm, clip, T, G, G ? 1 : 0, vec_x, vec_y,
                           XState{}, s);
   }
-  return run_general<S>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
+  if (norm) return run_general<S, true>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
+  return run_general<S, false>(x, y, B, n, ld_x, ld_y, p, clip, T, ws, vec_x, vec_y, s);
 }
 
 }  // namespace
@@ -729,19 +777,25 @@ int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t
   DSP_REQUIRE((ld_xs & 3) == 0 && (reinterpret_cast<uintptr_t>(xs) & 15) == 0 && ld_xs >= n_in,
               "x-domain states need 16-byte aligned SRC input rows");
   SosParams p;
-  for (int k = 0; k < DSP_MAX_STAGES; ++k)
-    for (int i = 0; i < 5; ++i) p.c[k][i] = (k < S) ? sos[5 * k + i] : (i == 0 ? 1.0 : 0.0);
+  DSP_REQUIRE(realize(sos, S, &p), "x-domain states need every b0 != 0");
   const int vec_x = ((ld_x & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0);
   const int vec_y = ((ld_y & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0);
   const int64_t T = chunk_len;
   switch (S) {
-    case 1: return run_fused<1>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 2: return run_fused<2>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 3: return run_fused<3>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 4: return run_fused<4>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 5: return run_fused<5>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 6: return run_fused<6>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
-    case 8: return run_fused<8>(x, y, B, n, ld_x, ld_y, p, clip, T, gx, 2, vec_x, vec_y, XS, s);
+    case 1: return run_fused<1>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 2: return run_fused<2>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 3: return run_fused<3>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 4: return run_fused<4>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 5: return run_fused<5>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 6: return run_fused<6>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
+    case 8: return run_fused<8>(x, y, B, n, ld_x, ld_y, p, true, clip, T, gx, 2, vec_x, vec_y,
+                                    XS, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
 }
@@ -763,28 +817,26 @@ int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
   if (B == 0 || n == 0) return DSP_OK;
   DSP_REQUIRE(x && y, "null pointer");
   DSP_REQUIRE(S == 0 || sos, "null sos");
-  // Pad S up to an instantiated size with exact identity stages (b = 1,0,0; a = 0,0).
+  // Pad S up to an instantiated size with exact identity stages.
   const int Sp = padded_stages(S);
   SosParams p;
-  for (int k = 0; k < DSP_MAX_STAGES; ++k) {
-    for (int i = 0; i < 5; ++i) p.c[k][i] = (k < S) ? sos[5 * k + i] : (i == 0 ? 1.0 : 0.0);
-  }
+  const bool norm = realize(sos, S, &p);
   const size_t need = ws_layout(B, n, Sp, chunk_len).total;
   DSP_REQUIRE(ws_bytes >= need, "workspace too small: %zu < %zu bytes", ws_bytes, need);
   DSP_REQUIRE(need == 0 || ws, "null workspace");
   // The state-response table is laid out for exactly S stages.
   const double* G = (Sp == S) ? state_table : nullptr;
   switch (Sp) {
-    case 0: return run_cascade<0>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 1: return run_cascade<1>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 2: return run_cascade<2>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 3: return run_cascade<3>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 4: return run_cascade<4>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 5: return run_cascade<5>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 6: return run_cascade<6>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 8: return run_cascade<8>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 12: return run_cascade<12>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
-    case 16: return run_cascade<16>(x, y, B, n, ld_x, ld_y, p, clip, chunk_len, G, ws, s);
+    case 0: return run_cascade<0>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 1: return run_cascade<1>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 2: return run_cascade<2>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 3: return run_cascade<3>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 4: return run_cascade<4>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 5: return run_cascade<5>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 6: return run_cascade<6>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 8: return run_cascade<8>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 12: return run_cascade<12>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
+    case 16: return run_cascade<16>(x, y, B, n, ld_x, ld_y, p, norm, clip, chunk_len, G, ws, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
 }

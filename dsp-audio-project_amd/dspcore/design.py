@@ -165,19 +165,44 @@ def chunk_len_for(n: int, max_chunks: int = 64) -> int:
     return max(32, -(-per // 32) * 32)
 
 
-def state_space(sos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
-    """(A, B) of the S-stage DF2T cascade as one D = 2S state system
-    X' = A X + B u, state order (s1_0, s2_0, s1_1, s2_1, ...)."""
+def df2_realization(sos: np.ndarray) -> tuple[np.ndarray, float, bool]:
+    """The kernels' realisation of a [S][5] {b0 b1 b2 a1 a2} cascade
+    (csrc/iir.hip:realize): direct form II per stage, rows {g, c1, c2, a1, a2}
+    and an input gain G.  With every b0 != 0 (NORM): g = 1, c = b/b0,
+    G = prod(b0); otherwise g = b0, c = (b1, b2), G = 1."""
     sos = np.asarray(sos, dtype=np.float64).reshape(-1, 5)
-    S = sos.shape[0]
+    norm = bool(np.all(sos[:, 0] != 0))
+    rows = np.empty_like(sos)
+    if norm:
+        rows[:, 0] = 1.0
+        rows[:, 1] = sos[:, 1] / sos[:, 0]
+        rows[:, 2] = sos[:, 2] / sos[:, 0]
+        gain = float(np.prod(sos[:, 0])) if sos.shape[0] else 1.0
+    else:
+        rows[:, :3] = sos[:, :3]
+        gain = 1.0
+    rows[:, 3:] = sos[:, 3:]
+    return rows, gain, norm
+
+
+def state_space(sos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """(A, B) of the S-stage cascade as one D = 2S state system X' = A X + B u
+    in the kernels' realisation (df2_realization), state order
+    (w1_0, w2_0, w1_1, w2_1, ...): the delay lines of each stage."""
+    rows, gain, norm = df2_realization(sos)
+    S = rows.shape[0]
     D = 2 * S
 
     def step(X, u):
         X = X.copy()
+        if norm:
+            u = gain * u
         for k in range(S):
-            b0, b1, b2, a1, a2 = sos[k]
-            v = b0 * u + X[2 * k]
-            X[2 * k], X[2 * k + 1] = b1 * u - a1 * v + X[2 * k + 1], b2 * u - a2 * v
+            g, c1, c2, a1, a2 = rows[k]
+            w = u - a1 * X[2 * k] - a2 * X[2 * k + 1]
+            v = g * w + c1 * X[2 * k] + c2 * X[2 * k + 1]
+            X[2 * k + 1] = X[2 * k]
+            X[2 * k] = w
             u = v
         return X
 

@@ -90,18 +90,44 @@ def test_shard_ranges_cover_batch_contiguously():
             assert len(r) <= parts
 
 
-def _cascade_end_state(sos, u):
-    """Reference DF2T recursion (lfilter's form) returning the final stage states."""
-    S = sos.shape[0]
+def _cascade_run(sos, u):
+    """The kernels' direct-form-II realisation (design.df2_realization),
+    written out independently: returns (outputs, final delay lines)."""
+    rows, gain, norm = design.df2_realization(sos)
+    S = rows.shape[0]
     st = np.zeros(2 * S)
-    for x in u:
-        v = x
+    out = np.empty(len(u))
+    for i, x in enumerate(u):
+        v = gain * x if norm else x
         for k in range(S):
-            b0, b1, b2, a1, a2 = sos[k]
-            out = b0 * v + st[2 * k]
-            st[2 * k], st[2 * k + 1] = b1 * v - a1 * out + st[2 * k + 1], b2 * v - a2 * out
-            v = out
-    return st
+            g, c1, c2, a1, a2 = rows[k]
+            w = v - a1 * st[2 * k] - a2 * st[2 * k + 1]
+            v = g * w + c1 * st[2 * k] + c2 * st[2 * k + 1]
+            st[2 * k + 1] = st[2 * k]
+            st[2 * k] = w
+        out[i] = v
+    return out, st
+
+
+def test_df2_realisation_matches_lfilter():
+    """The rearranged recursion computes the reference's lfilter cascade
+    (dsp_core.py:205-214, :233-251) to float64 rounding, with and without the
+    b0 normalisation (a stage with b0 == 0 keeps its gain)."""
+    from scipy.signal import lfilter
+    sos = design.eq_plan(72000, {"Sub-Bass": 15, "Bass": -9, "Low Mids": 3, "Presence": 6,
+                                 "Brilliance": -6}).sos
+    u = np.random.default_rng(3).uniform(-1, 1, 3000)
+    ref = u.copy()
+    for row in sos:
+        ref = lfilter(row[:3], np.r_[1.0, row[3:]], ref)
+    got, _ = _cascade_run(sos, u)
+    assert design.df2_realization(sos)[2]
+    assert np.max(np.abs(got - ref)) <= 1e-11
+    odd = np.array([[0.0, 0.5, -0.25, -1.2, 0.5]])
+    assert not design.df2_realization(odd)[2]
+    got, _ = _cascade_run(odd, u)
+    np.testing.assert_allclose(got, lfilter([0.0, 0.5, -0.25], [1.0, -1.2, 0.5], u),
+                               rtol=0, atol=1e-12)
 
 
 def test_state_response_table_gives_chunk_end_states():
@@ -111,7 +137,8 @@ def test_state_response_table_gives_chunk_end_states():
         u = rng.uniform(-1, 1, T)
         G = design.state_response_table(sos, T)
         assert G.shape == (T, 2 * sos.shape[0])
-        np.testing.assert_allclose(u @ G, _cascade_end_state(sos, u), rtol=0, atol=1e-11)
+        end = _cascade_run(sos, u)[1]
+        np.testing.assert_allclose(u @ G, end, rtol=1e-10, atol=1e-9)
 
 
 def test_chunk_policy_is_batch_independent_and_fused():

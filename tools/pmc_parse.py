@@ -12,17 +12,23 @@ import re
 import sys
 from collections import defaultdict
 
-SHORT = [("k_src_state", "src_state"), ("k_src", "src_poly"), ("k_iir_fused<6, 2", "iir_apply"), ("k_iir_fused", "iir_fused"), ("k_iir_pass<", "iir_pass"),
-         ("k_iir_carry", "iir_carry"), ("k_iir_prep", "iir_prep"), ("k_spectrum", "spectrum"),
-         ("k_fft_c2c", "fft")]
-
-
 def short(name):
-    for key, s in SHORT:
-        if key in name:
-            if s == "iir_pass":
-                return "iir_apply" if "true" in name.split("k_iir_pass<")[1][:12] else "iir_state"
-            return s
+    """Bench-trace name of a libdspcore kernel from its demangled symbol."""
+    if "k_src" in name:
+        return "src_poly"
+    m = re.search(r"k_iir_wave<(\d+), (\d+)", name)
+    if m:
+        return "iir_xstate" if m.group(2) == "2" else "iir_fused"
+    m = re.search(r"k_iir_pass<(\d+), (true|false)", name)
+    if m:
+        return "iir_apply" if m.group(2) == "true" else "iir_state"
+    if "k_iir_carry" in name:
+        return "iir_carry"
+    if "k_iir_prep" in name:
+        return "iir_prep"
+    m = re.search(r"k_fft<(\d+), (\d+)", name)
+    if m:
+        return "spectrum" if m.group(2) == "2" else "fft"
     return None
 
 
