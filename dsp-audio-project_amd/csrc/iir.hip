@@ -753,7 +753,9 @@ int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* 
   auto floor_div = [](int64_t a, int64_t d) { return a >= 0 ? a / d : -((-a + d - 1) / d); };
   const int64_t qmax = floor_div((chunk_len - 1) * M + c, L);
   const int64_t qmin = -floor_div(K - 1 - c, L);  // ceil((c - K + 1) / L)
-  const int64_t lo = floor_div(qmin, 4) * 4;
+  // Row starts c*shift + q0 on 128-byte boundaries when shift is a multiple of
+  // 32 (config 3): a misaligned 128-byte row segment costs two cache lines.
+  const int64_t lo = floor_div(qmin, 32) * 32;
   const int64_t span = qmax - lo + 1;
   *shift = sh;
   *q0 = lo;

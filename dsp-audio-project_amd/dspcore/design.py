@@ -231,12 +231,21 @@ def state_response_table(sos: np.ndarray, chunk_len: int) -> np.ndarray:
 def xstate_chunk_len(n_out: int, L: int, M: int, max_chunks: int = 64) -> int:
     """Chunk length for the chain's x-domain chunk states (include/dspcore.h,
     dsp_chain_f32): the smallest multiple of 32 with chunk_len*M/L an integer
-    multiple of 4 that splits n_out into <= max_chunks chunks.  A function of
-    (n_out, L, M) only, so rows stay independent of the batch size."""
-    unit = 4 * L // math.gcd(M, 4 * L)          # chunk_len*M % (4L) == 0
-    step = 32 * unit // math.gcd(32, unit)      # lcm(32, unit)
+    multiple of 32 (128-byte aligned x rows) that splits n_out into between
+    max_chunks/2 and max_chunks chunks, else the smallest with chunk_len*M/L a
+    multiple of 4.  A function of (n_out, L, M) only, so rows stay independent
+    of the batch size."""
     per = -(-int(n_out) // max_chunks)
-    return max(step, -(-per // step) * step)
+    best = None
+    for q in (32, 4):   # prefer 128-byte aligned chunk rows of x (csrc/iir.hip)
+        unit = q * L // math.gcd(M, q * L)      # chunk_len*M % (qL) == 0
+        step = 32 * unit // math.gcd(32, unit)  # lcm(32, unit)
+        T = max(step, -(-per // step) * step)
+        if best is None or T < best:
+            best = T
+        if -(-int(n_out) // T) >= max_chunks // 2:  # keeps >= half the chunk lanes
+            return T
+    return best
 
 
 def xstate_table(sos: np.ndarray, plan: "SrcPlan", chunk_len: int, q0: int,

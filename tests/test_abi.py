@@ -75,7 +75,7 @@ def test_xstate_geometry_query():
     refs = [ctypes.byref(o) for o in out]
     assert lib.dsp_chain_xstate_geometry(1152, 121, 3, 2, 60, *refs) == 0
     shift, q0, rows = (o.value for o in out)
-    assert shift == 768 and q0 % 4 == 0 and rows % 32 == 0
+    assert shift == 768 and q0 % 32 == 0 and rows % 32 == 0
     assert q0 <= -((121 - 1 - 60) // 3) and q0 + rows > (1151 * 2 + 60) // 3
     # chunk_len*M not a multiple of L, or a shift that is not a multiple of 4
     assert lib.dsp_chain_xstate_geometry(1000, 121, 3, 2, 60, *refs) == _lib.DSP_EINVAL

@@ -20,6 +20,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 cat "$OUT/kernel_stats.csv" | cut -d, -f1-8 | head -12
 echo "== pmc"
+mkdir -p "$OUT/pmc"
 i=0
 while read -r group; do
   [ -z "$group" ] && continue
