@@ -104,6 +104,15 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                               window, twiddles, static_cast<hipStream_t>(stream));
 }
 
+int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
+                     int64_t seg_len, int64_t hop, int64_t frames, int32_t log2n,
+                     int64_t ld_mag, const float* window, const float* twiddles,
+                     void* stream) {
+  dsp::clear_error();
+  return dsp::launch_stft(x, mag, B, ld_x, seg_start, seg_len, hop, frames, log2n, ld_mag,
+                          window, twiddles, static_cast<hipStream_t>(stream));
+}
+
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
   return dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
 }

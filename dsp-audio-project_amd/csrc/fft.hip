@@ -28,6 +28,8 @@
 // exp(-2*pi*i*k/N), k < N/2 (rounded to fp32), and w_r = w1^r by at most four
 // complex products (error ~4 ulp, far inside the 1e-5 tolerance).
 // Small transforms (N < 4096) pack 256 / (N/16) transforms per workgroup.
+// The spectrum mode also runs a framed STFT: transform t = (row, frame) reads
+// the window-weighted frame starting hop*frame samples into the row's segment.
 #include "common.h"
 
 namespace dsp {
@@ -146,22 +148,41 @@ __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 struct FftArgs {
   const float* in;     // real rows (kR2C, kSpec) or interleaved complex rows (kC2C)
   float* out;          // complex rows (kC2C, kR2C) or magnitudes (kSpec)
-  int64_t B, ld_in, ld_out;
-  int64_t seg_start, seg_len;  // kSpec
-  const float* win;            // kSpec
-  const float2* tw;            // exp(-2 pi i k / N), k < N/2
+  int64_t B, ld_in, ld_out;      // B = transforms (rows x frames for kSpec)
+  int64_t seg_start, seg_len;    // kSpec: valid samples [seg_start, seg_start + seg_len)
+  int64_t hop, frames;           // kSpec: frame f of a row starts hop*f after seg_start
+  const float* win;              // kSpec
+  const float2* tw;              // exp(-2 pi i k / N), k < N/2
 };
 
-// Value n of transform t as the first pass reads it.
+// Where transform t reads its input: element n is in[base + n] (complex or real
+// element units); kSpec frames also carry their valid length.
+struct InRow {
+  int64_t base;
+  int64_t valid;  // kSpec: samples of the frame inside the segment
+};
+
 template <int MODE>
-__device__ __forceinline__ float2 load_input(const FftArgs& a, int64_t t, int n, bool live) {
+__device__ __forceinline__ InRow in_row(const FftArgs& a, int64_t t) {
+  if constexpr (MODE == kSpec) {
+    const int64_t row = a.frames == 1 ? t : t / a.frames;
+    const int64_t f0 = (t - row * a.frames) * a.hop;  // frame start within the segment
+    return InRow{row * a.ld_in + a.seg_start + f0, a.seg_len - f0};
+  } else {
+    return InRow{t * a.ld_in, 0};
+  }
+}
+
+// Value n of the transform as the first pass reads it.
+template <int MODE>
+__device__ __forceinline__ float2 load_input(const FftArgs& a, const InRow& r, int n, bool live) {
   if (!live) return make_float2(0.f, 0.f);
   if constexpr (MODE == kC2C) {
-    return reinterpret_cast<const float2*>(a.in)[t * a.ld_in + n];
+    return reinterpret_cast<const float2*>(a.in)[r.base + n];
   } else if constexpr (MODE == kR2C) {
-    return make_float2(a.in[t * a.ld_in + n], 0.f);
+    return make_float2(a.in[r.base + n], 0.f);
   } else {
-    const float s = (n < a.seg_len) ? a.in[t * a.ld_in + a.seg_start + n] : 0.f;
+    const float s = (n < r.valid) ? a.in[r.base + n] : 0.f;
     return make_float2(s * a.win[n], 0.f);
   }
 }
@@ -204,8 +225,9 @@ __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restri
 }
 
 template <int LOG2N, int MODE, int P>
-__device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t t, int j0,
-                                         bool live, const Tw<LOG2N, P - 1 < 0 ? 0 : P - 1>& tw) {
+__device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t t,
+                                         const InRow& ir, int j0, bool live,
+                                         const Tw<LOG2N, P - 1 < 0 ? 0 : P - 1>& tw) {
   using PL = Plan<LOG2N>;
   constexpr int N = PL::N;
   constexpr int R = PL::radix(P);
@@ -220,7 +242,7 @@ __device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int n = j + r * STRIDE;
-      v[b][r] = FIRST ? load_input<MODE>(a, t, n, live) : buf[lpad(n)];
+      v[b][r] = FIRST ? load_input<MODE>(a, ir, n, live) : buf[lpad(n)];
     }
   }
   if constexpr (!FIRST) __syncthreads();  // every read of this pass precedes its writes
@@ -247,8 +269,8 @@ __device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t 
   }
   if constexpr (!LAST) __syncthreads();
   if constexpr (P + 1 < PL::NP) {
-    if constexpr (P == 0) run_pass<LOG2N, MODE, P + 1>(a, buf, t, j0, live, tw);
-    else run_pass<LOG2N, MODE, P + 1>(a, buf, t, j0, live, tw.next);
+    if constexpr (P == 0) run_pass<LOG2N, MODE, P + 1>(a, buf, t, ir, j0, live, tw);
+    else run_pass<LOG2N, MODE, P + 1>(a, buf, t, ir, j0, live, tw.next);
   }
 }
 
@@ -260,12 +282,13 @@ __global__ __launch_bounds__(Plan<LOG2N>::NT) void k_fft(FftArgs a) {
   const int j0 = threadIdx.x - tl * PL::TPT;
   const int64_t t = (int64_t)blockIdx.x * PL::TPB + tl;
   const bool live = t < a.B;
+  const InRow ir = in_row<MODE>(a, live ? t : 0);
   if constexpr (PL::NP == 0) {
-    store_output<MODE, 1>(a, t, 0, load_input<MODE>(a, t, 0, live), live);
+    store_output<MODE, 1>(a, t, 0, load_input<MODE>(a, ir, 0, live), live);
   } else {
     Tw<LOG2N, 0> tw;
     load_tw<LOG2N, 0>(tw, a.tw, j0);
-    run_pass<LOG2N, MODE, 0>(a, lds + tl * PL::PADN, t, j0, live, tw);
+    run_pass<LOG2N, MODE, 0>(a, lds + tl * PL::PADN, t, ir, j0, live, tw);
   }
 }
 
@@ -308,19 +331,28 @@ int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,
                     hipStream_t s) {
+  return launch_stft(x, mag, B, ld_x, seg_start, seg_len, 0, 1, log2n, ld_mag, window, tw, s);
+}
+
+int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
+                int64_t seg_len, int64_t hop, int64_t frames, int log2n, int64_t ld_mag,
+                const float* window, const float* tw, hipStream_t s) {
   DSP_REQUIRE(log2n >= 0 && log2n <= DSP_MAX_LOG2N, "log2n=%d outside [0, %d]", log2n,
               DSP_MAX_LOG2N);
   const int64_t N = int64_t(1) << log2n;
-  DSP_REQUIRE(B >= 0 && seg_start >= 0 && seg_len >= 0 && seg_len <= N,
+  DSP_REQUIRE(frames >= 1 && hop >= 0 && (frames == 1 || hop >= 1), "bad framing hop=%lld "
+              "frames=%lld", (long long)hop, (long long)frames);
+  DSP_REQUIRE(B >= 0 && seg_start >= 0 && seg_len >= 0 && (frames > 1 || seg_len <= N),
               "bad segment start=%lld len=%lld (N=%lld)", (long long)seg_start,
               (long long)seg_len, (long long)N);
   DSP_REQUIRE(ld_mag >= N / 2 + 1, "ld_mag too small");
   DSP_REQUIRE(ld_x >= seg_start + seg_len, "segment exceeds the row");
   if (B == 0) return DSP_OK;
   DSP_REQUIRE(x && mag && window && tw, "null pointer");
-  FftArgs a{x, mag, B, ld_x, ld_mag, seg_start, seg_len, window,
+  DSP_REQUIRE(B <= INT64_MAX / frames, "too many frames");
+  FftArgs a{x, mag, B * frames, ld_x, ld_mag, seg_start, seg_len, hop, frames, window,
             reinterpret_cast<const float2*>(tw)};
-  TraceScope trace("spectrum", s);
+  TraceScope trace(frames == 1 ? "spectrum" : "stft", s);
   return dispatch<kSpec>(a, log2n, s);
 }
 
@@ -335,7 +367,7 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
                   (real_in || (reinterpret_cast<uintptr_t>(in) & 7) == 0),
               "complex buffers must be 8-byte aligned");
-  FftArgs a{in, out, B, ld_in, ld_out, 0, 0, nullptr, reinterpret_cast<const float2*>(tw)};
+  FftArgs a{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, reinterpret_cast<const float2*>(tw)};
   TraceScope trace("fft", s);
   return real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s);
 }

@@ -49,6 +49,9 @@ _SIGNATURES = {
     "dsp_spectrum_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp,
         _vp]),
+    "dsp_stft_mag_f32": (ctypes.c_int, [
+        _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp,
+        _vp]),
     "dsp_chain_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,

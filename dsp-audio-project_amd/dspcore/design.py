@@ -308,6 +308,29 @@ def spectrum_plan(length: int, window: int = SPECTRUM_WINDOW) -> SpectrumPlan:
     return SpectrumPlan(start, seg, n)
 
 
+@dataclass(frozen=True)
+class StftPlan:
+    n_fft: int
+    hop: int
+    frames: int
+
+
+def stft_plan(length: int, n_fft: int = SPECTRUM_WINDOW, hop: int | None = None) -> StftPlan:
+    """Framing of the spectrogram extension: frames of
+    n_fft samples (a power of two, as the reference's FFT requires) every `hop`
+    samples (default n_fft // 4) from the start of the signal; every frame that
+    starts inside the signal while the previous one did not reach its end, i.e.
+    1 + ceil(max(0, length - n_fft) / hop) frames, the last zero-padded."""
+    n_fft = int(n_fft)
+    if n_fft < 1 or n_fft & (n_fft - 1):
+        raise ValueError(f"n_fft={n_fft} is not a power of two; the radix-2 FFT needs 2^k points")
+    hop = max(1, n_fft // 4) if hop is None else int(hop)
+    if hop < 1:
+        raise ValueError("hop must be >= 1")
+    frames = 1 + -(-max(0, int(length) - n_fft) // hop)
+    return StftPlan(n_fft, hop, frames)
+
+
 def hann(n: int) -> np.ndarray:
     """Window of dsp_core.py:85-87: 0.5 - 0.5 cos(2 pi n / (N - 1)), float64."""
     k = np.arange(n)

@@ -226,3 +226,27 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
                                   lg, ld(out), _ptr(win), _ptr(tw), _stream(x.device))
     _lib.check(rc, "dsp_spectrum_f32")
     return out
+
+
+def stft_magnitude(x: torch.Tensor, n_fft: int, hop: int, frames: int,
+                   out: torch.Tensor | None = None) -> torch.Tensor:
+    """|FFT(hann * frame)|[:n_fft/2+1] of every frame x[b, f*hop : f*hop + n_fft]
+    (zero-padded past the row's end) -> [B, frames, n_fft/2+1] float32."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    B, n = x.shape
+    lg = _log2(n_fft)
+    half = n_fft // 2 + 1
+    if out is None:
+        out = torch.empty((B, frames, half), dtype=torch.float32, device=x.device)
+    if B == 0:
+        return out
+    win = _table("hann", n_fft, x.device)
+    tw = _table("tw", n_fft, x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_stft_mag_f32(_ptr(x), _ptr(out), B, ld(x), 0, n, hop, frames, lg,
+                                  out.stride(1), _ptr(win), _ptr(tw), _stream(x.device))
+    _lib.check(rc, "dsp_stft_mag_f32")
+    return out

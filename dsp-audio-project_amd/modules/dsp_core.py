@@ -26,7 +26,8 @@ Deliberate differences, documented in DESIGN.md:
   power of two (the reference raises for most and returns a wrong-length
   array for N = 3);
 * keyword-only extensions: conversion_tasa_muestreo(..., num_taps=None) and
-  calcular_espectro_magnitud(..., n_fft=2048).
+  calcular_espectro_magnitud(..., n_fft=2048); one added function,
+  calcular_espectrograma_magnitud (every frame).
 """
 from __future__ import annotations
 
@@ -38,7 +39,7 @@ __all__ = [
     "cargar_senal_audio", "fft_diezmado_en_tiempo", "calcular_espectro_magnitud",
     "generar_respuesta_impulso_sinc", "conversion_tasa_muestreo",
     "disenar_coeficientes_diferencias", "aplicar_ecuacion_diferencias",
-    "sistema_ecualizador",
+    "sistema_ecualizador", "calcular_espectrograma_magnitud",
 ]
 
 
@@ -187,6 +188,23 @@ def calcular_espectro_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW)
     half = plan.n_fft // 2 + 1
     freqs = np.fft.rfftfreq(plan.n_fft, d=1 / fs)[:half]
     return freqs, _from_rows(mag, how, np.float64)
+
+
+def calcular_espectrograma_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW,
+                                    hop: int | None = None):
+    """Extension (not in the reference): the recipe of calcular_espectro_magnitud
+    (Hann window of dsp_core.py:87, FFT, |X[k]| for k <= N/2) applied to every
+    frame of the signal instead of its centre segment.  Frames of n_fft samples
+    every `hop` (default n_fft // 4) from the start, the last zero-padded
+    (design.stft_plan).  Returns (frequencies [N/2+1], frame start times in
+    seconds [frames], magnitudes [frames, N/2+1] -- or [B, frames, N/2+1])."""
+    plan = _design.stft_plan(_length(x_n), n_fft, hop)
+    ops = _ops()
+    t, how = _to_rows(x_n)
+    mag = ops.stft_magnitude(t, plan.n_fft, plan.hop, plan.frames)
+    freqs = np.fft.rfftfreq(plan.n_fft, d=1 / fs)[:plan.n_fft // 2 + 1]
+    times = np.arange(plan.frames) * plan.hop / fs
+    return freqs, times, _from_rows(mag, how, np.float64)
 
 
 # ---------------------------------------------------------------------------

@@ -111,6 +111,18 @@ int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                      const float* twiddles, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Framed magnitude spectrogram (every frame instead of
+ * calcular_espectro_magnitud's centre segment, dsp_core.py:74-98).
+ * Frame f < `frames` of row b is x[b][seg_start + f*hop + j], j < N = 2^log2n,
+ * zero past seg_start + seg_len; mag[(b*frames + f)*ld_mag + k] =
+ * |FFT(window * frame)[k]| for k <= N/2.  frames == 1 is dsp_spectrum_f32.
+ * ------------------------------------------------------------------------- */
+int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
+                     int64_t seg_start, int64_t seg_len, int64_t hop, int64_t frames,
+                     int32_t log2n, int64_t ld_mag, const float* window,
+                     const float* twiddles, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Whole hot path of app.py:164-167 + :203-205 for a batch of channels:
  *   y   = SRC(x)                     (dsp_src_polyphase_f32)
  *   z   = clip(cascade(y))           (dsp_biquad_cascade_f32; S == 0 and

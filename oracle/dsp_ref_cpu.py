@@ -52,6 +52,20 @@ def spectrum(x, fs, window=2048):
     return np.fft.rfftfreq(n, d=1 / fs)[:keep], mag[:keep]
 
 
+def spectrogram(x, n_fft, hop, frames):
+    """The spectrum recipe of reference dsp_core.py:85-97 (Hann window
+    0.5 - 0.5 cos(2 pi n / (N - 1)), radix-2 DIT FFT, |X[k]| for k <= N/2)
+    applied to frames x[f*hop : f*hop + n_fft], zero-padded past the end."""
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n_fft) / (n_fft - 1))
+    out = np.empty((frames, n_fft // 2 + 1))
+    for f in range(frames):
+        seg = np.zeros(n_fft)
+        part = x[f * hop:f * hop + n_fft]
+        seg[:len(part)] = part
+        out[f] = np.abs(fft_dit(seg * w))[:n_fft // 2 + 1]
+    return out
+
+
 def sinc_taps(wc, num_taps):
     """Windowed-sinc low-pass normalised to unit sum (reference dsp_core.py:104-131)."""
     if num_taps % 2 == 0:

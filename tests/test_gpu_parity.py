@@ -234,6 +234,32 @@ def test_spectrum_matches_reference(gpu):
                 dc.calcular_espectro_magnitud(np.ones(int(n)), 44100)
 
 
+def test_stft_frames_match_reference_recipe(gpu):
+    """Every frame of the spectrogram extension equals the reference's spectrum
+    recipe (Hann, radix-2 FFT, |X|) on that frame: max|d| <= 1e-5 * max|X|
+    per frame; ragged last frame zero-padded; one frame when n < n_fft."""
+    from oracle import dsp_ref_cpu as orc
+    dc = _dc()
+    rng = np.random.default_rng(11)
+    for n, n_fft, hop in [(10000, 1024, 256), (4096, 4096, 1000), (3000, 4096, 512),
+                          (9999, 256, 100), (72000, 2048, 512)]:
+        x = rng.uniform(-1, 1, (2, n))
+        f, times, mag = dc.calcular_espectrograma_magnitud(x, 72000, n_fft=n_fft, hop=hop)
+        frames = 1 + -(-max(0, n - n_fft) // hop)
+        assert mag.shape == (2, frames, n_fft // 2 + 1) and mag.dtype == np.float64
+        assert f.shape == (n_fft // 2 + 1,) and times.shape == (frames,)
+        for b in range(2):
+            ref = orc.spectrogram(x[b].astype(np.float32).astype(np.float64), n_fft, hop, frames)
+            err = np.max(np.abs(mag[b] - ref), axis=1)
+            assert np.all(err <= FFT_RTOL * np.maximum(np.max(ref, axis=1), 1e-30)), (n, n_fft)
+    # frames == 1 on the centre segment is the spectrum kernel itself
+    x = rng.uniform(-1, 1, (1, 72000)).astype(np.float32)
+    xt = torch.from_numpy(x).to(gpu)
+    one = _ops().stft_magnitude(xt[:, 36000:36000 + 4096].contiguous(), 4096, 4096, 1)
+    spec = _ops().spectrum(xt, 36000, 4096, 4096)
+    assert torch.equal(one[:, 0], spec)
+
+
 # --------------------------------------------------------------------------- chain
 @pytest.mark.parametrize("tag,fs,L,M,K", [("c3", 48000, 3, 2, None),
                                           ("c5", 44100, 160, 147, 1023)])

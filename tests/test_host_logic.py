@@ -181,3 +181,12 @@ def test_xstate_table_reproduces_output_domain_states():
             xv = np.where((idx >= 0) & (idx < n_in), x[np.clip(idx, 0, n_in - 1)], 0.0)
             e_x = gx.T @ xv
             assert np.max(np.abs(e_x - e_y)) <= 1e-12 * max(1.0, np.max(np.abs(e_y)))
+
+
+def test_stft_plan_framing():
+    assert design.stft_plan(10000, 1024, 256) == design.StftPlan(1024, 256, 1 + 36)
+    assert design.stft_plan(1024, 1024).frames == 1
+    assert design.stft_plan(100, 1024).frames == 1            # zero-padded single frame
+    assert design.stft_plan(72000, 2048).hop == 512
+    with pytest.raises(ValueError):
+        design.stft_plan(1000, 1000)
