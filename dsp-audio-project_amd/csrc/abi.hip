@@ -149,6 +149,39 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                               twiddles, s);
 }
 
+int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info) {
+  dsp::clear_error();
+  return dsp::wav_parse(file, len, info);
+}
+
+int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t channels,
+                        int64_t B, int64_t frames, int64_t ld_bytes, float* out,
+                        int64_t ld_out, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_pcm_mono(pcm, format, bits, channels, B, frames, ld_bytes, out, ld_out,
+                              static_cast<hipStream_t>(stream));
+}
+
+int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
+                           uint32_t* peak_out, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_peak_normalize(x, B, n, ld, threshold, peak_out,
+                                    static_cast<hipStream_t>(stream));
+}
+
+int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
+                       int64_t ld_out, uint32_t* peak_out, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_quantize_pcm16(z, out, B, n, ld_z, ld_out, peak_out,
+                                    static_cast<hipStream_t>(stream));
+}
+
+int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,
+                         int64_t frames) {
+  dsp::clear_error();
+  return dsp::wav_header_pcm16(header44, sample_rate, channels, frames);
+}
+
 int dsp_trace_enable(int32_t enable) {
   dsp::clear_error();
   dsp::g_trace.on = enable != 0;

@@ -1,0 +1,296 @@
+// Audio I/O edges of the hot path, gfx950.
+//
+// Loader: reference modules/dsp_core.py:10-35 (cargar_senal_audio) reads the
+// file with soundfile (float64, integers scaled by 2^-(bits-1), unsigned 8-bit
+// offset by 128), averages the channels (x_n.mean(axis=1), float64), casts to
+// float32 and divides by max|x| when that exceeds 1e-6.  Here the host parses
+// the RIFF/WAVE header (dsp_wav_parse, no sample touched), the raw PCM bytes go
+// to the GPU as they are (2 bytes per 16-bit sample instead of 8 for float64),
+// and two kernels finish the job:
+//   k_pcm_mono:   decode + channel mean in float64 (numpy's summation order),
+//                 rounded to float32 -- bit-identical to the reference;
+//   k_absmax:     per-row max|x| as an unsigned max over float bits (NaN sorts
+//                 above +inf, so a NaN peak propagates like np.max);
+//   k_scale:      x /= peak (IEEE float32 division) where peak > threshold.
+// Playback: reference app.py:349-355 turns z into 16-bit PCM: nan_to_num,
+// divide by max|z| if > 0, * 32767, astype(int16) (truncation), all float64.
+// k_quantize16 does exactly that per row from the float32 z the chain wrote.
+// Everything is HBM-streaming integer/byte work: coalesced loads, one pass.
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+namespace dsp {
+namespace {
+
+constexpr int kIoNT = 256;
+
+// Sample c of frame i as soundfile returns it (float64).
+template <int FMT, int BITS>
+__device__ __forceinline__ double decode(const uint8_t* __restrict__ p) {
+  if constexpr (FMT == DSP_WAV_FLOAT) {
+    if constexpr (BITS == 32) {
+      float f;
+      memcpy(&f, p, 4);
+      return (double)f;
+    } else {
+      double d;
+      memcpy(&d, p, 8);
+      return d;
+    }
+  } else if constexpr (BITS == 8) {
+    return ((double)p[0] - 128.0) / 128.0;
+  } else if constexpr (BITS == 16) {
+    const int16_t v = (int16_t)(p[0] | (p[1] << 8));
+    return (double)v / 32768.0;
+  } else if constexpr (BITS == 24) {
+    int32_t v = p[0] | (p[1] << 8) | (p[2] << 16);
+    v = (v << 8) >> 8;  // sign-extend
+    return (double)v / 8388608.0;
+  } else {
+    const int32_t v = (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) |
+                                ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+    return (double)v / 2147483648.0;
+  }
+}
+
+// np.add.reduce over a contiguous axis of length ch, then / ch: a plain loop
+// below 8 elements, numpy's 8-accumulator pairwise block up to 128.
+template <int FMT, int BITS>
+__device__ __forceinline__ double channel_mean(const uint8_t* __restrict__ f, int ch) {
+  constexpr int W = BITS / 8;
+  if (ch == 1) return decode<FMT, BITS>(f);
+  double s;
+  if (ch < 8) {
+    s = decode<FMT, BITS>(f);
+    for (int c = 1; c < ch; ++c) s += decode<FMT, BITS>(f + c * W);
+  } else {
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = decode<FMT, BITS>(f + k * W);
+    int c = 8;
+    for (; c + 8 <= ch; c += 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] += decode<FMT, BITS>(f + (c + k) * W);
+    }
+    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; c < ch; ++c) s += decode<FMT, BITS>(f + c * W);
+  }
+  return s / (double)ch;
+}
+
+template <int FMT, int BITS>
+__global__ __launch_bounds__(kIoNT) void k_pcm_mono(const uint8_t* __restrict__ pcm, int ch,
+                                                   int64_t frames, int64_t ld_bytes,
+                                                   float* __restrict__ out, int64_t ld_out) {
+  const int64_t b = blockIdx.y;
+  const uint8_t* row = pcm + b * ld_bytes;
+  float* o = out + b * ld_out;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < frames; i += stride)
+    o[i] = (float)channel_mean<FMT, BITS>(row + i * (int64_t)ch * (BITS / 8), ch);
+}
+
+// Row max of |x| as float bits (all non-negative, so unsigned order is float
+// order, with NaN above +inf).  NAN0: NaN counts as 0 (np.nan_to_num first).
+template <bool NAN0>
+__global__ __launch_bounds__(kIoNT) void k_absmax(const float* __restrict__ x, int64_t n,
+                                                 int64_t ld, uint32_t* __restrict__ peak) {
+  const int64_t b = blockIdx.y;
+  const float* r = x + b * ld;
+  uint32_t m = 0;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < n; i += stride) {
+    uint32_t u = __float_as_uint(r[i]) & 0x7fffffffu;
+    if (NAN0 && u > 0x7f800000u) u = 0;
+    m = max(m, u);
+  }
+  // wave reduction, then one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(peak + b, m);
+}
+
+__global__ __launch_bounds__(kIoNT) void k_scale(float* __restrict__ x, int64_t n, int64_t ld,
+                                                const uint32_t* __restrict__ peak,
+                                                double threshold) {
+  const int64_t b = blockIdx.y;
+  const float pk = __uint_as_float(peak[b]);
+  if (!((double)pk > threshold)) return;  // NaN peak: unchanged, as in the reference
+  float* r = x + b * ld;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < n; i += stride)
+    r[i] = r[i] / pk;
+}
+
+__global__ __launch_bounds__(kIoNT) void k_quantize16(const float* __restrict__ z, int64_t n,
+                                                     int64_t ld_z, int16_t* __restrict__ out,
+                                                     int64_t ld_out,
+                                                     const uint32_t* __restrict__ peak) {
+  const int64_t b = blockIdx.y;
+  const uint32_t pu = peak[b];
+  // nan_to_num maps +-inf to +-DBL_MAX, so an infinite peak is DBL_MAX.
+  const double pk = pu == 0x7f800000u ? DBL_MAX : (double)__uint_as_float(pu);
+  const float* r = z + b * ld_z;
+  int16_t* o = out + b * ld_out;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < n; i += stride) {
+    double v = (double)r[i];
+    if (v != v) v = 0.0;
+    else if (v == INFINITY) v = DBL_MAX;
+    else if (v == -INFINITY) v = -DBL_MAX;
+    if (pk > 0.0) v /= pk;
+    o[i] = (int16_t)(int)(v * 32767.0);  // truncation toward zero, |v * 32767| <= 32767
+  }
+}
+
+unsigned io_blocks(int64_t n) {
+  const int64_t want = ceil_div(n, (int64_t)kIoNT * 4);  // ~4 elements per thread
+  return (unsigned)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
+}
+
+int absmax(const float* x, int64_t B, int64_t n, int64_t ld, uint32_t* peak, bool nan0,
+           hipStream_t s) {
+  DSP_HIP(hipMemsetAsync(peak, 0, (size_t)B * sizeof(uint32_t), s));
+  if (n == 0) return DSP_OK;
+  const dim3 grid(io_blocks(n), (unsigned)B);
+  if (nan0)
+    hipLaunchKernelGGL(k_absmax<true>, grid, dim3(kIoNT), 0, s, x, n, ld, peak);
+  else
+    hipLaunchKernelGGL(k_absmax<false>, grid, dim3(kIoNT), 0, s, x, n, ld, peak);
+  DSP_LAUNCHED("k_absmax");
+  return DSP_OK;
+}
+
+uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+void wr32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+
+}  // namespace
+
+int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
+  DSP_REQUIRE(buf && info, "null pointer");
+  DSP_REQUIRE(len >= 12 && !memcmp(buf, "RIFF", 4) && !memcmp(buf + 8, "WAVE", 4),
+              "not a RIFF/WAVE file");
+  bool have_fmt = false;
+  int tag = 0;
+  dsp_wav_info w{};
+  size_t pos = 12;
+  while (pos + 8 <= len) {
+    const uint32_t sz = rd32(buf + pos + 4);
+    const uint8_t* body = buf + pos + 8;
+    const size_t avail = len - (pos + 8);
+    if (!memcmp(buf + pos, "fmt ", 4)) {
+      DSP_REQUIRE(sz >= 16 && avail >= 16, "truncated fmt chunk");
+      tag = rd16(body);
+      w.channels = rd16(body + 2);
+      w.sample_rate = (int32_t)rd32(body + 4);
+      w.bits = rd16(body + 14);
+      if (tag == 0xFFFE) {  // WAVE_FORMAT_EXTENSIBLE: the sub-format GUID starts with the tag
+        DSP_REQUIRE(sz >= 40 && avail >= 26, "truncated extensible fmt chunk");
+        tag = rd16(body + 24);
+      }
+      have_fmt = true;
+    } else if (!memcmp(buf + pos, "data", 4)) {
+      DSP_REQUIRE(have_fmt, "data chunk before fmt chunk");
+      w.data_offset = (int64_t)(pos + 8);
+      // A streamed header may carry a size past the end: read what is there.
+      w.data_bytes = (int64_t)(sz <= avail ? sz : avail);
+      break;
+    }
+    pos += 8 + (size_t)sz + (sz & 1);  // chunks are word aligned
+  }
+  DSP_REQUIRE(have_fmt && w.data_offset > 0, "no fmt/data chunk");
+  DSP_REQUIRE(w.channels >= 1 && w.channels <= 128, "channels=%d outside [1, 128]", w.channels);
+  if (tag == 1) {
+    w.format = DSP_WAV_PCM;
+    DSP_REQUIRE(w.bits == 8 || w.bits == 16 || w.bits == 24 || w.bits == 32,
+                "unsupported PCM width %d", w.bits);
+  } else if (tag == 3) {
+    w.format = DSP_WAV_FLOAT;
+    DSP_REQUIRE(w.bits == 32 || w.bits == 64, "unsupported float width %d", w.bits);
+  } else {
+    return set_error(DSP_EINVAL, "unsupported WAVE format tag %d", tag);
+  }
+  w.frames = w.data_bytes / ((int64_t)w.channels * (w.bits / 8));
+  *info = w;
+  return DSP_OK;
+}
+
+int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames) {
+  DSP_REQUIRE(out && fs > 0 && channels >= 1 && frames >= 0, "bad header arguments");
+  const int64_t data = frames * channels * 2;
+  DSP_REQUIRE(data + 36 <= (int64_t)UINT32_MAX, "data too large for RIFF");
+  memcpy(out, "RIFF", 4);
+  wr32(out + 4, (uint32_t)(36 + data));
+  memcpy(out + 8, "WAVEfmt ", 8);
+  wr32(out + 16, 16);
+  wr16(out + 20, 1);
+  wr16(out + 22, (uint16_t)channels);
+  wr32(out + 24, (uint32_t)fs);
+  wr32(out + 28, (uint32_t)(fs * channels * 2));
+  wr16(out + 32, (uint16_t)(channels * 2));
+  wr16(out + 34, 16);
+  memcpy(out + 36, "data", 4);
+  wr32(out + 40, (uint32_t)data);
+  return DSP_OK;
+}
+
+int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t B,
+                    int64_t frames, int64_t ld_bytes, float* out, int64_t ld_out, hipStream_t s) {
+  DSP_REQUIRE(B >= 0 && frames >= 0 && channels >= 1 && channels <= 128, "bad sizes");
+  DSP_REQUIRE(ld_bytes >= frames * channels * (bits / 8) && ld_out >= frames,
+              "leading dimension too small");
+  if (B == 0 || frames == 0) return DSP_OK;
+  DSP_REQUIRE(pcm && out, "null pointer");
+  const uint8_t* p = static_cast<const uint8_t*>(pcm);
+  const dim3 grid(io_blocks(frames), (unsigned)B);
+#define DSP_PCM(F, BI)                                                                        \
+  if (format == F && bits == BI) {                                                            \
+    hipLaunchKernelGGL((k_pcm_mono<F, BI>), grid, dim3(kIoNT), 0, s, p, channels, frames,   \
+                       ld_bytes, out, ld_out);                                                \
+    DSP_LAUNCHED("k_pcm_mono");                                                               \
+    return DSP_OK;                                                                            \
+  }
+  DSP_PCM(DSP_WAV_PCM, 8)
+  DSP_PCM(DSP_WAV_PCM, 16)
+  DSP_PCM(DSP_WAV_PCM, 24)
+  DSP_PCM(DSP_WAV_PCM, 32)
+  DSP_PCM(DSP_WAV_FLOAT, 32)
+  DSP_PCM(DSP_WAV_FLOAT, 64)
+#undef DSP_PCM
+  return set_error(DSP_EINVAL, "unsupported sample format %d / %d bits", format, bits);
+}
+
+int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
+                          uint32_t* peak, hipStream_t s) {
+  DSP_REQUIRE(B >= 0 && n >= 0 && ld >= n, "bad sizes");
+  if (B == 0) return DSP_OK;
+  DSP_REQUIRE(x && peak, "null pointer");
+  TraceScope trace("peak_normalize", s);
+  if (int rc = absmax(x, B, n, ld, peak, false, s)) return rc;
+  if (n == 0) return DSP_OK;
+  hipLaunchKernelGGL(k_scale, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, x, n, ld,
+                     peak, threshold);
+  DSP_LAUNCHED("k_scale");
+  return DSP_OK;
+}
+
+int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
+                          int64_t ld_out, uint32_t* peak, hipStream_t s) {
+  DSP_REQUIRE(B >= 0 && n >= 0 && ld_z >= n && ld_out >= n, "bad sizes");
+  if (B == 0) return DSP_OK;
+  DSP_REQUIRE(z && out && peak, "null pointer");
+  TraceScope trace("quantize16", s);
+  if (int rc = absmax(z, B, n, ld_z, peak, true, s)) return rc;
+  if (n == 0) return DSP_OK;
+  hipLaunchKernelGGL(k_quantize16, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z, n,
+                     ld_z, out, ld_out, peak);
+  DSP_LAUNCHED("k_quantize16");
+  return DSP_OK;
+}
+
+}  // namespace dsp

@@ -91,6 +91,16 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 // Fused cascade whose chunk end states E[B][C-1][2S] were produced upstream.
+// Audio I/O (audio_io.hip).
+int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
+int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames);
+int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t B,
+                    int64_t frames, int64_t ld_bytes, float* out, int64_t ld_out, hipStream_t s);
+int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
+                          uint32_t* peak, hipStream_t s);
+int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
+                          int64_t ld_out, uint32_t* peak, hipStream_t s);
+
 // Chain fast path: pass 1 of the fused cascade reads the SRC input xs through
 // the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,

@@ -60,10 +60,27 @@ _SIGNATURES = {
     "dsp_chain_xstate_geometry": (ctypes.c_int, [
         _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64),
         ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
+    "dsp_wav_parse": (ctypes.c_int, [ctypes.c_char_p, _c_sz, _vp]),
+    "dsp_pcm_to_mono_f32": (ctypes.c_int, [
+        _vp, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
+    "dsp_peak_normalize_f32": (ctypes.c_int, [
+        _vp, _c_i64, _c_i64, _c_i64, ctypes.c_double, _vp, _vp]),
+    "dsp_quantize_pcm16": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp]),
+    "dsp_wav_header_pcm16": (ctypes.c_int, [ctypes.c_char_p, _c_i32, _c_i32, _c_i64]),
     "dsp_trace_enable": (ctypes.c_int, [_c_i32]),
     "dsp_trace_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _c_i32]),
 }
 DSP_TRACE_NAME = 32
+DSP_WAV_PCM = 1
+DSP_WAV_FLOAT = 3
+
+
+class WavInfo(ctypes.Structure):
+    """dsp_wav_info of include/dspcore.h."""
+    _fields_ = [("format", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("sample_rate", ctypes.c_int32), ("bits", ctypes.c_int32),
+                ("frames", ctypes.c_int64), ("data_offset", ctypes.c_int64),
+                ("data_bytes", ctypes.c_int64)]
 
 _lock = threading.Lock()
 _lib = None

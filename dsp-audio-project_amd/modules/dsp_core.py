@@ -97,62 +97,25 @@ def _length(x) -> int:
 
 
 # ---------------------------------------------------------------------------
-# I/O (out of the kernel scope; kept for the module surface, app.py:14)
+# I/O (app.py:14)
 # ---------------------------------------------------------------------------
-def _read_audio(source):
-    try:
-        import soundfile as sf  # the reference's loader (dsp_core.py:20)
-        return sf.read(source)
-    except ImportError:
-        pass
-    # soundfile is not installed in this image: decode PCM WAV with the stdlib
-    # and scale integers the way soundfile does (float64 in [-1, 1)).
-    import io
-    import wave
-    src = source
-    if hasattr(source, "read") and not hasattr(source, "seek"):
-        src = io.BytesIO(source.read())
-    with wave.open(src, "rb") as w:
-        fs = w.getframerate()
-        ch = w.getnchannels()
-        width = w.getsampwidth()
-        raw = w.readframes(w.getnframes())
-    if width == 1:
-        data = (np.frombuffer(raw, np.uint8).astype(np.float64) - 128.0) / 128.0
-    elif width == 2:
-        data = np.frombuffer(raw, "<i2").astype(np.float64) / 32768.0
-    elif width == 3:
-        b = np.frombuffer(raw, np.uint8).reshape(-1, 3)
-        v = (b[:, 0].astype(np.int32) | (b[:, 1].astype(np.int32) << 8)
-             | (b[:, 2].astype(np.int32) << 16))
-        v = np.where(v >= 1 << 23, v - (1 << 24), v)
-        data = v.astype(np.float64) / float(1 << 23)
-    elif width == 4:
-        data = np.frombuffer(raw, "<i4").astype(np.float64) / float(1 << 31)
-    else:
-        raise ValueError(f"unsupported sample width {width}")
-    if ch > 1:
-        data = data.reshape(-1, ch)
-    return data, fs
-
-
 def cargar_senal_audio(buffer_archivo):
     """Load x[n]: read, average to mono, float32, peak-normalise (dsp_core.py:10-35).
 
-    Any failure returns (zeros(100, float32), 44100), as the reference's bare
-    `except` does (:34-35).
+    The WAV header is parsed on the host; decoding, the channel mean and the
+    peak normalisation run on the GPU with the reference's arithmetic
+    (dspcore/audio_io.py).  Any failure to read or decode returns
+    (zeros(100, float32), 44100), as the reference's bare `except` does
+    (:34-35); a missing GPU or library still raises RuntimeError.
     """
+    from dspcore import audio_io
     try:
-        x_n, fs = _read_audio(buffer_archivo)
-        if len(x_n.shape) > 1:
-            x_n = x_n.mean(axis=1)
-        x_n = x_n.astype(np.float32)
-        peak = np.max(np.abs(x_n))
-        if peak > 1e-6:
-            x_n = x_n / peak
-        return x_n, fs
+        x, fs = audio_io.load(buffer_archivo)
+    except RuntimeError:
+        raise
     except Exception:
         return np.zeros(100, dtype=np.float32), 44100
+    return x.cpu().numpy(), fs
 
 
 # ---------------------------------------------------------------------------

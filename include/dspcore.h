@@ -160,6 +160,54 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Audio I/O edges.
+ *
+ * Loader, replacing dsp_core.py:10-35 (cargar_senal_audio: soundfile read,
+ * channel mean, float32, divide by max|x| when > 1e-6):
+ *   dsp_wav_parse        HOST: RIFF/WAVE header of an in-memory file (PCM 8/16/
+ *                        24/32-bit, IEEE float 32/64, WAVE_FORMAT_EXTENSIBLE);
+ *                        no sample is touched;
+ *   dsp_pcm_to_mono_f32  DEVICE: raw interleaved sample bytes [B][ld_bytes] ->
+ *                        float32 [B][ld_out]: each sample scaled as soundfile
+ *                        returns it (float64: ints / 2^(bits-1), u8 - 128), the
+ *                        channel mean in float64 in numpy's summation order,
+ *                        rounded to float32 (bit-identical to the reference);
+ *   dsp_peak_normalize_f32  DEVICE: per row, peak = max|x| (float32; a NaN
+ *                        propagates like np.max) and x /= peak where
+ *                        (double)peak > threshold (the reference uses 1e-6).
+ *                        peak_out: caller's device uint32[B], receives the
+ *                        peaks as float32 bit patterns.
+ * Playback, replacing app.py:349-355 (nan_to_num, divide by max|z| when > 0,
+ * * 32767, astype(int16), all float64):
+ *   dsp_quantize_pcm16   DEVICE: float32 z [B][ld_z] -> int16 [B][ld_out],
+ *                        peak_out as above (after nan_to_num);
+ *   dsp_wav_header_pcm16 HOST: the 44-byte header scipy.io.wavfile.write puts
+ *                        in front of 16-bit PCM (app.py:352).
+ * ------------------------------------------------------------------------- */
+#define DSP_WAV_PCM 1    /* integer PCM (8-bit unsigned, 16/24/32-bit signed) */
+#define DSP_WAV_FLOAT 3  /* IEEE float, 32 or 64 bits                           */
+typedef struct dsp_wav_info {
+  int32_t format;       /* DSP_WAV_PCM or DSP_WAV_FLOAT                  */
+  int32_t channels;     /* interleaved channels, 1..128                  */
+  int32_t sample_rate;  /* Hz                                            */
+  int32_t bits;         /* bits per sample                               */
+  int64_t frames;       /* samples per channel in the data chunk         */
+  int64_t data_offset;  /* byte offset of the first sample in the file   */
+  int64_t data_bytes;   /* bytes of sample data present                  */
+} dsp_wav_info;
+
+int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info);
+int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t channels,
+                        int64_t B, int64_t frames, int64_t ld_bytes, float* out,
+                        int64_t ld_out, void* stream);
+int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
+                           uint32_t* peak_out, void* stream);
+int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
+                       int64_t ld_out, uint32_t* peak_out, void* stream);
+int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,
+                         int64_t frames);
+
+/* ---------------------------------------------------------------------------
  * Per-launch tracing (the reference has no tracing; this is the build's).
  * While enabled on the calling thread, every kernel this thread launches
  * through the library is bracketed by two hipEventRecord calls on its stream

@@ -21,6 +21,45 @@ BANDS = (("Sub-Bass", 40), ("Bass", 150), ("Low Mids", 1000),
          ("High Mids", 3000), ("Presence", 5000), ("Brilliance", 10000))
 
 
+def load_audio(data):
+    """cargar_senal_audio (reference dsp_core.py:10-35) on WAV bytes, with
+    scipy.io.wavfile.read standing in for soundfile (absent here) and
+    soundfile's documented float64 scaling restated: integer PCM / 2^(bits-1)
+    (24-bit arrives as int32 << 8, so / 2^31), unsigned 8-bit (v - 128) / 128,
+    float as stored.  Parity of that scaling is unpinned (no reference audio
+    ships: .MISSING_LARGE_BLOBS); the mean / cast / normalise are the
+    reference's own numpy calls."""
+    import io
+
+    from scipy.io import wavfile
+    fs, raw = wavfile.read(io.BytesIO(data))
+    if raw.dtype == np.uint8:
+        x = (raw.astype(np.float64) - 128.0) / 128.0
+    elif raw.dtype == np.int16:
+        x = raw.astype(np.float64) / 32768.0
+    elif raw.dtype == np.int32:
+        x = raw.astype(np.float64) / 2147483648.0
+    else:
+        x = raw.astype(np.float64)
+    if len(x.shape) > 1:
+        x = x.mean(axis=1)
+    x = x.astype(np.float32)
+    peak = np.max(np.abs(x))
+    if peak > 1e-6:
+        x = x / peak
+    return x, fs
+
+
+def playback_pcm16(z):
+    """app.py:349-355: nan_to_num, divide by the peak when > 0, * 32767,
+    astype(int16), in float64."""
+    y = np.nan_to_num(np.asarray(z, dtype=np.float64))
+    peak = np.max(np.abs(y))
+    if peak > 0:
+        y /= peak
+    return (y * 32767).astype(np.int16)
+
+
 def fft_dit(x):
     """Recursive radix-2 DIT FFT (reference dsp_core.py:41-66).
 

@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 13
+    assert len(names) == 18
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -80,3 +80,53 @@ def test_xstate_geometry_query():
     # chunk_len*M not a multiple of L, or a shift that is not a multiple of 4
     assert lib.dsp_chain_xstate_geometry(1000, 121, 3, 2, 60, *refs) == _lib.DSP_EINVAL
     assert lib.dsp_chain_xstate_geometry(1149, 121, 3, 2, 60, *refs) == _lib.DSP_EINVAL
+
+
+def _wav(fmt_tag, channels, rate, bits, payload, extensible=False, extra_chunk=False):
+    import struct
+    block = channels * bits // 8
+    if extensible:
+        fmt = struct.pack("<HHIIHH", 0xFFFE, channels, rate, rate * block, block, bits)
+        fmt += struct.pack("<HHI", 22, bits, 0) + struct.pack("<H", fmt_tag) + bytes(14)
+    else:
+        fmt = struct.pack("<HHIIHH", fmt_tag, channels, rate, rate * block, block, bits)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt
+    if extra_chunk:   # odd-sized chunk: padded to a word boundary
+        body += b"LIST" + struct.pack("<I", 3) + b"abc" + b"\0"
+    body += b"data" + struct.pack("<I", len(payload)) + payload
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def test_wav_parse_host_only():
+    """dsp_wav_parse reads headers without a GPU: PCM, float, extensible,
+    chunks before data; rejects what soundfile would not give as PCM/float."""
+    lib = _lib.load()
+    info = _lib.WavInfo()
+    f = _wav(1, 2, 44100, 16, bytes(400), extra_chunk=True)
+    assert lib.dsp_wav_parse(f, len(f), ctypes.byref(info)) == 0
+    assert (info.format, info.channels, info.sample_rate, info.bits, info.frames) == \
+        (_lib.DSP_WAV_PCM, 2, 44100, 16, 100)
+    assert f[info.data_offset - 8:info.data_offset - 4] == b"data"
+    f = _wav(3, 1, 48000, 32, bytes(64), extensible=True)
+    assert lib.dsp_wav_parse(f, len(f), ctypes.byref(info)) == 0
+    assert (info.format, info.bits, info.frames) == (_lib.DSP_WAV_FLOAT, 32, 16)
+    f = _wav(1, 1, 8000, 24, bytes(30))
+    assert lib.dsp_wav_parse(f, len(f), ctypes.byref(info)) == 0 and info.frames == 10
+    for bad in (b"RIFX" + bytes(40), _wav(2, 1, 8000, 4, bytes(8)), _wav(1, 1, 8000, 12, bytes(8)),
+                b"RIFF\x04\0\0\0WAVE"):
+        assert lib.dsp_wav_parse(bad, len(bad), ctypes.byref(info)) == _lib.DSP_EINVAL
+
+
+def test_wav_header_matches_scipy_writer():
+    """The playback header is byte-identical to scipy.io.wavfile.write's for
+    int16 (what app.py:352 calls)."""
+    import io
+
+    import numpy as np
+    from scipy.io import wavfile
+    pcm = (np.arange(-500, 500) * 31).astype(np.int16)
+    buf = io.BytesIO()
+    wavfile.write(buf, 72000, pcm)
+    hdr = ctypes.create_string_buffer(44)
+    assert _lib.load().dsp_wav_header_pcm16(hdr, 72000, 1, pcm.size) == 0
+    assert hdr.raw + pcm.tobytes() == buf.getvalue()

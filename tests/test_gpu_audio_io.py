@@ -1,0 +1,105 @@
+"""Loader and playback edges on the GPU, bitwise
+against the oracle's restatement of dsp_core.py:10-35 and app.py:349-355."""
+import io
+import struct
+
+import numpy as np
+import pytest
+import torch
+from scipy.io import wavfile
+
+pytestmark = pytest.mark.gpu
+
+
+def _wavfile(x, rate):
+    buf = io.BytesIO()
+    wavfile.write(buf, rate, x)
+    return buf.getvalue()
+
+
+def _wav24(ints, channels, rate):
+    """24-bit PCM (scipy cannot write it): little-endian 3-byte samples."""
+    v = np.asarray(ints, dtype=np.int32).reshape(-1)
+    b = np.stack([(v >> s) & 0xFF for s in (0, 8, 16)], axis=1).astype(np.uint8).tobytes()
+    block = 3 * channels
+    fmt = struct.pack("<HHIIHH", 1, channels, rate, rate * block, block, 24)
+    body = b"WAVEfmt " + struct.pack("<I", 16) + fmt + b"data" + struct.pack("<I", len(b)) + b
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def _oracle_24(ints, channels):
+    x = np.asarray(ints, dtype=np.float64).reshape(-1, channels) / 8388608.0
+    x = x.mean(axis=1) if channels > 1 else x[:, 0]
+    x = x.astype(np.float32)
+    peak = np.max(np.abs(x))
+    return x / peak if peak > 1e-6 else x
+
+
+def test_loader_matches_reference_bitwise(gpu):
+    from modules import dsp_core
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(5)
+    cases = {
+        "int16 stereo": rng.integers(-32768, 32767, (4001, 2), dtype=np.int16),
+        "int16 mono": rng.integers(-9000, 9000, 3000, dtype=np.int16),
+        "uint8 stereo": rng.integers(0, 255, (2000, 2), dtype=np.uint8),
+        "int32 mono": rng.integers(-2**31, 2**31 - 1, 1500, dtype=np.int32),
+        "float32 stereo": rng.uniform(-0.7, 0.7, (2500, 2)).astype(np.float32),
+        "float64 5ch": rng.uniform(-2, 2, (1200, 5)),
+        "float32 10ch": rng.uniform(-1, 1, (700, 10)).astype(np.float32),
+        "silence": np.zeros((500, 2), dtype=np.int16),
+        "tiny": (rng.uniform(-1, 1, 600) * 1e-7).astype(np.float32),
+    }
+    for name, arr in cases.items():
+        data = _wavfile(arr, 44100)
+        x, fs = dsp_core.cargar_senal_audio(io.BytesIO(data))
+        ref, rfs = orc.load_audio(data)
+        assert fs == rfs and x.dtype == np.float32 and x.shape == ref.shape, name
+        np.testing.assert_array_equal(x, ref, err_msg=name)
+    ints = rng.integers(-2**23, 2**23 - 1, (900, 2))
+    x, fs = dsp_core.cargar_senal_audio(_wav24(ints, 2, 48000))
+    np.testing.assert_array_equal(x, _oracle_24(ints, 2))
+    # unreadable input: the reference's fallback
+    x, fs = dsp_core.cargar_senal_audio(io.BytesIO(b"not audio at all"))
+    assert fs == 44100 and x.dtype == np.float32 and np.array_equal(x, np.zeros(100))
+
+
+def test_loader_batch_rows_equal_single_loads(gpu):
+    from dspcore import audio_io
+    rng = np.random.default_rng(6)
+    files = [_wavfile(rng.integers(-30000, 30000, (n, 2), dtype=np.int16), 48000)
+             for n in (1000, 2500, 1777)]
+    batch, lengths, rates = audio_io.load_batch(files, gpu)
+    assert lengths == [1000, 2500, 1777] and rates == [48000] * 3
+    for i, f in enumerate(files):
+        one, _ = audio_io.load(f, gpu)
+        assert torch.equal(batch[i, :lengths[i]], one)
+        assert not batch[i, lengths[i]:].any()
+
+
+def test_peak_normalize_nan_and_threshold(gpu):
+    from dspcore import audio_io
+    x = torch.tensor([[0.5, -2.0, 1.0], [float("nan"), 3.0, 1.0], [1e-7, -5e-7, 0.0]],
+                     device=gpu)
+    peaks = audio_io.peak_normalize(x)
+    assert peaks[0].item() == 2.0 and torch.isnan(peaks[1])
+    assert x[0].tolist() == [0.25, -1.0, 0.5]
+    assert x[1, 1].item() == 3.0 and x[2, 1].item() == np.float32(-5e-7)  # unchanged
+
+
+def test_playback_quantization_matches_app_bitwise(gpu):
+    from dspcore import audio_io
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(8)
+    z = rng.uniform(-1, 1, (4, 5000)).astype(np.float32)
+    z[1, 10] = np.nan
+    z[2, :] = 0.0
+    z[3, 7] = np.inf
+    z[3, 8] = -np.inf
+    q = audio_io.quantize_pcm16(torch.from_numpy(z).to(gpu)).cpu().numpy()
+    for b in range(4):
+        np.testing.assert_array_equal(q[b], orc.playback_pcm16(z[b]))
+    wav = audio_io.wav_bytes_pcm16(torch.from_numpy(z[0]).to(gpu), 72000)
+    buf = io.BytesIO()
+    wavfile.write(buf, 72000, orc.playback_pcm16(z[0]))
+    assert wav == buf.getvalue()
