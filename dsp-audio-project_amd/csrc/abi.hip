@@ -95,6 +95,21 @@ int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                          static_cast<hipStream_t>(stream));
 }
 
+int dsp_dft_size(int64_t n) {
+  dsp::clear_error();
+  if (n < 1 || n > DSP_MAX_DFT) return dsp::set_error(DSP_EINVAL, "n=%lld outside [1, %d]",
+                                                      (long long)n, DSP_MAX_DFT);
+  return 1 << dsp::bluestein_log2m(n);
+}
+
+int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_input,
+                int64_t ld_in, int64_t ld_out, const float* chirp, const float* chirp_fft,
+                const float* twiddles_m, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_dft(in, out, B, n, real_input, ld_in, ld_out, chirp, chirp_fft, twiddles_m,
+                         static_cast<hipStream_t>(stream));
+}
+
 int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                      int64_t seg_start, int64_t seg_len, int32_t log2n,
                      int64_t ld_mag, const float* window,

@@ -224,9 +224,24 @@ __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restri
   }
 }
 
-template <int LOG2N, int MODE, int P>
-__device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t t,
-                                         const InRow& ir, int j0, bool live,
+// IO policies of a transform: load(n) feeds the first pass, store(k, v) takes
+// the last pass's natural-order output.  kLdsIn: load() reads the LDS buffer
+// the passes work in, so the first pass also waits before writing.
+template <int MODE, int N>
+struct GlobalIO {
+  static constexpr bool kLdsIn = false;
+  const FftArgs& a;
+  InRow ir;
+  int64_t t;
+  bool live;
+  __device__ __forceinline__ float2 load(int n) const { return load_input<MODE>(a, ir, n, live); }
+  __device__ __forceinline__ void store(int k, float2 v) const {
+    store_output<MODE, N>(a, t, k, v, live);
+  }
+};
+
+template <int LOG2N, int P, class IO>
+__device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
                                          const Tw<LOG2N, P - 1 < 0 ? 0 : P - 1>& tw) {
   using PL = Plan<LOG2N>;
   constexpr int N = PL::N;
@@ -242,10 +257,11 @@ __device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int n = j + r * STRIDE;
-      v[b][r] = FIRST ? load_input<MODE>(a, ir, n, live) : buf[lpad(n)];
+      v[b][r] = FIRST ? io.load(n) : buf[lpad(n)];
     }
   }
-  if constexpr (!FIRST) __syncthreads();  // every read of this pass precedes its writes
+  // every read of this pass precedes its (in-place) writes
+  if constexpr (!FIRST || IO::kLdsIn) __syncthreads();
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int j = j0 + b * PL::TPT;
@@ -263,14 +279,14 @@ __device__ __forceinline__ void run_pass(const FftArgs& a, float2* buf, int64_t 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = base + r * NS;
-      if constexpr (LAST) store_output<MODE, N>(a, t, k, v[b][r], live);
+      if constexpr (LAST) io.store(k, v[b][r]);
       else buf[lpad(k)] = v[b][r];
     }
   }
   if constexpr (!LAST) __syncthreads();
   if constexpr (P + 1 < PL::NP) {
-    if constexpr (P == 0) run_pass<LOG2N, MODE, P + 1>(a, buf, t, ir, j0, live, tw);
-    else run_pass<LOG2N, MODE, P + 1>(a, buf, t, ir, j0, live, tw.next);
+    if constexpr (P == 0) run_pass<LOG2N, P + 1>(io, buf, j0, tw);
+    else run_pass<LOG2N, P + 1>(io, buf, j0, tw.next);
   }
 }
 
@@ -282,14 +298,96 @@ __global__ __launch_bounds__(Plan<LOG2N>::NT) void k_fft(FftArgs a) {
   const int j0 = threadIdx.x - tl * PL::TPT;
   const int64_t t = (int64_t)blockIdx.x * PL::TPB + tl;
   const bool live = t < a.B;
-  const InRow ir = in_row<MODE>(a, live ? t : 0);
+  const GlobalIO<MODE, PL::N> io{a, in_row<MODE>(a, live ? t : 0), t, live};
   if constexpr (PL::NP == 0) {
-    store_output<MODE, 1>(a, t, 0, load_input<MODE>(a, ir, 0, live), live);
+    io.store(0, io.load(0));
   } else {
     Tw<LOG2N, 0> tw;
     load_tw<LOG2N, 0>(tw, a.tw, j0);
-    run_pass<LOG2N, MODE, 0>(a, lds + tl * PL::PADN, t, ir, j0, live, tw);
+    run_pass<LOG2N, 0>(io, lds + tl * PL::PADN, j0, tw);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Any-length DFT by Bluestein's chirp-z identity (for app.py:322-324, whose
+// np.fft.fft segments have length int(1024 * L/M), e.g. 1114 = 2 * 557):
+//   w[k] = exp(-i pi k^2 / n),  X[k] = w[k] * sum_j (x[j] w[j]) conj(w[k-j]),
+// a circular convolution of length M = 2^m >= 2n - 1 done as two M-point
+// Stockham transforms in one workgroup's LDS:
+//   A = FFT(x w, zero-padded);  D = FFT(conj(A * Bf));  X[k] = w[k] conj(D[k])
+// with Bf = FFT(b)/M, b[j] = b[M-j] = conj(w[j]) (j < n), from the host in
+// float64 (rounded to float32).  The 1/M of the inverse transform is in Bf.
+// ---------------------------------------------------------------------------
+struct BluArgs {
+  const float* in;   // real rows or interleaved complex rows
+  float* out;        // interleaved complex rows, n values
+  int64_t B, n, ld_in, ld_out;
+  int real_in;
+  const float2* chirp;  // w[k], k < n
+  const float2* bf;     // FFT_M(b) / M
+  const float2* tw;     // exp(-2 pi i k / M), k < M/2
+};
+
+template <int N>
+struct BluStage1 {
+  static constexpr bool kLdsIn = false;
+  const BluArgs& a;
+  float2* buf;
+  int64_t t;
+  bool live;
+  __device__ __forceinline__ float2 load(int j) const {
+    if (!live || j >= a.n) return make_float2(0.f, 0.f);
+    const float2 x = a.real_in ? make_float2(a.in[t * a.ld_in + j], 0.f)
+                               : reinterpret_cast<const float2*>(a.in)[t * a.ld_in + j];
+    return cmul(x, a.chirp[j]);
+  }
+  __device__ __forceinline__ void store(int k, float2 v) const {
+    const float2 c = cmul(v, a.bf[k]);
+    buf[lpad(k)] = make_float2(c.x, -c.y);
+  }
+};
+
+template <int N>
+struct BluStage2 {
+  static constexpr bool kLdsIn = true;
+  const BluArgs& a;
+  float2* buf;
+  int64_t t;
+  bool live;
+  __device__ __forceinline__ float2 load(int j) const { return buf[lpad(j)]; }
+  __device__ __forceinline__ void store(int k, float2 v) const {
+    if (live && k < a.n)
+      reinterpret_cast<float2*>(a.out)[t * a.ld_out + k] =
+          cmul(make_float2(v.x, -v.y), a.chirp[k]);
+  }
+};
+
+template <int LOG2N>
+__global__ __launch_bounds__(Plan<LOG2N>::NT) void k_bluestein(BluArgs a) {
+  using PL = Plan<LOG2N>;
+  static_assert(PL::NP >= 1, "Bluestein needs M >= 2");
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int tl = threadIdx.x / PL::TPT;
+  const int j0 = threadIdx.x - tl * PL::TPT;
+  const int64_t t = (int64_t)blockIdx.x * PL::TPB + tl;
+  const bool live = t < a.B;
+  float2* buf = lds + tl * PL::PADN;
+  Tw<LOG2N, 0> tw;
+  load_tw<LOG2N, 0>(tw, a.tw, j0);
+  run_pass<LOG2N, 0>(BluStage1<PL::N>{a, buf, t, live}, buf, j0, tw);
+  __syncthreads();  // stage 1's last pass wrote LDS
+  run_pass<LOG2N, 0>(BluStage2<PL::N>{a, buf, t, live}, buf, j0, tw);
+}
+
+template <int LOG2N>
+int launch_blu(const BluArgs& a, hipStream_t s) {
+  using PL = Plan<LOG2N>;
+  const size_t shm = (size_t)PL::TPB * PL::PADN * sizeof(float2);
+  if (int rc = allow_lds(k_bluestein<LOG2N>, shm)) return rc;
+  const unsigned grid = (unsigned)ceil_div(a.B, PL::TPB);
+  hipLaunchKernelGGL(k_bluestein<LOG2N>, dim3(grid), dim3(PL::NT), shm, s, a);
+  DSP_LAUNCHED("k_bluestein");
+  return DSP_OK;
 }
 
 template <int MODE, int LOG2N>
@@ -370,6 +468,48 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
   FftArgs a{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, reinterpret_cast<const float2*>(tw)};
   TraceScope trace("fft", s);
   return real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s);
+}
+
+}  // namespace dsp
+
+namespace dsp {
+
+int bluestein_log2m(int64_t n) {
+  int m = 1;
+  while ((int64_t(1) << m) < 2 * n - 1) ++m;
+  return m;
+}
+
+int launch_dft(const float* in, float* out, int64_t B, int64_t n, int real_in, int64_t ld_in,
+               int64_t ld_out, const float* chirp, const float* chirp_fft, const float* tw_m,
+               hipStream_t s) {
+  DSP_REQUIRE(n >= 1 && n <= DSP_MAX_DFT, "n=%lld outside [1, %d]", (long long)n, DSP_MAX_DFT);
+  DSP_REQUIRE(B >= 0 && ld_in >= n && ld_out >= n, "bad sizes");
+  if (B == 0) return DSP_OK;
+  DSP_REQUIRE(in && out && chirp && chirp_fft && tw_m, "null pointer");
+  DSP_REQUIRE((reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
+                  (real_in || (reinterpret_cast<uintptr_t>(in) & 7) == 0),
+              "complex buffers must be 8-byte aligned");
+  BluArgs a{in, out, B, n, ld_in, ld_out, real_in, reinterpret_cast<const float2*>(chirp),
+            reinterpret_cast<const float2*>(chirp_fft), reinterpret_cast<const float2*>(tw_m)};
+  TraceScope trace("dft", s);
+  switch (bluestein_log2m(n)) {
+    case 1: return launch_blu<1>(a, s);
+    case 2: return launch_blu<2>(a, s);
+    case 3: return launch_blu<3>(a, s);
+    case 4: return launch_blu<4>(a, s);
+    case 5: return launch_blu<5>(a, s);
+    case 6: return launch_blu<6>(a, s);
+    case 7: return launch_blu<7>(a, s);
+    case 8: return launch_blu<8>(a, s);
+    case 9: return launch_blu<9>(a, s);
+    case 10: return launch_blu<10>(a, s);
+    case 11: return launch_blu<11>(a, s);
+    case 12: return launch_blu<12>(a, s);
+    case 13: return launch_blu<13>(a, s);
+    case 14: return launch_blu<14>(a, s);
+    default: return set_error(DSP_EINVAL, "no Bluestein size for n=%lld", (long long)n);
+  }
 }
 
 }  // namespace dsp

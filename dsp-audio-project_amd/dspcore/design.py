@@ -342,3 +342,21 @@ def twiddles(n: int) -> np.ndarray:
     """exp(-2j pi k / N), k < N/2, computed in float64 (dsp_core.py:59-60)."""
     k = np.arange(max(n // 2, 1))
     return np.exp(-2j * np.pi * k / n)
+
+
+def bluestein_tables(n: int) -> tuple[np.ndarray, np.ndarray, int]:
+    """(chirp[n], FFT_M(b)/M [M], M) of the any-length DFT (include/dspcore.h,
+    dsp_dft_f32), float64: chirp[k] = exp(-i pi (k^2 mod 2n) / n) (the modulus
+    keeps the phase argument small and exact), b[j] = b[M-j] = conj(chirp[j])."""
+    n = int(n)
+    m = 1
+    while (1 << m) < 2 * n - 1:
+        m += 1
+    M = 1 << m
+    k = np.arange(n, dtype=np.int64)
+    chirp = np.exp(-1j * np.pi * ((k * k) % (2 * n)) / n)
+    b = np.zeros(M, dtype=np.complex128)
+    b[:n] = np.conj(chirp)
+    if n > 1:
+        b[M - np.arange(1, n)] = np.conj(chirp[1:])
+    return chirp, np.fft.fft(b) / M, M

@@ -178,6 +178,46 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     return out
 
 
+def _dft_tables(n: int, device: torch.device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    key = ("BLU", n, device.index)
+    t = _tables.get(key)
+    if t is None:
+        with _tables_lock:
+            t = _tables.get(key)
+            if t is None:
+                from .design import bluestein_tables
+                chirp, bf, M = bluestein_tables(n)
+                if M != _lib.load().dsp_dft_size(n):
+                    raise RuntimeError("Bluestein size mismatch between host and library")
+                t = tuple(torch.from_numpy(a.astype(np.complex64).view(np.float32)).to(device)
+                          for a in (chirp, bf)) + (_table("tw", M, device),)
+                _tables[key] = t
+    return t
+
+
+def dft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Natural-order DFT of every row for ANY length n <= 8192 (np.fft.fft's
+    contract, app.py:322-324), complex64: the radix-2 kernel for powers of two,
+    Bluestein (dsp_dft_f32) otherwise."""
+    x = _rows(x, "x")
+    B, n = x.shape
+    if n >= 1 and n & (n - 1) == 0 and n.bit_length() - 1 <= _lib.DSP_MAX_LOG2N:
+        return fft(x, out)
+    if n < 1 or n > _lib.DSP_MAX_DFT:
+        raise ValueError(f"DFT length {n} outside [1, {_lib.DSP_MAX_DFT}]")
+    real = not x.is_complex()
+    x = x.float() if real else x.to(torch.complex64)
+    if out is None:
+        out = torch.empty((B, n), dtype=torch.complex64, device=x.device)
+    chirp, bf, tw = _dft_tables(n, x.device)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_dft_f32(_ptr(x), _ptr(out), B, n, int(real), ld(x), ld(out), _ptr(chirp),
+                             _ptr(bf), _ptr(tw), _stream(x.device))
+    _lib.check(rc, "dsp_dft_f32")
+    return out
+
+
 def _log2(n: int) -> int:
     if n < 1 or n & (n - 1):
         raise ValueError(f"length {n} is not a power of two; the radix-2 FFT needs 2^k points")

@@ -37,6 +37,7 @@ extern "C" {
 
 #define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
+#define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
 
 /* ABI version (major*10000 + minor*100 + patch). */
 int dsp_version(void);
@@ -97,6 +98,23 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
 int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
                        const float* twiddles, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Any-length DFT, batched (app.py:322-324 calls
+ * np.fft.fft on segments of int(1024*L/M) samples, not powers of two).
+ * Bluestein: 1 <= n <= DSP_MAX_DFT, M = 2^m the smallest power of two
+ * >= 2n - 1 (dsp_dft_size).  Tables from the caller, float64-computed and
+ * rounded to float32, interleaved complex:
+ *   chirp[k]     = exp(-i pi (k^2 mod 2n) / n),            k < n
+ *   chirp_fft[k] = FFT_M(b)[k] / M, b[j] = b[M-j] = conj(chirp[j]) (j < n),
+ *                  0 elsewhere,                            k < M
+ *   twiddles_m   = exp(-2 pi i k / M),                     k < M/2
+ * in: real float32 [B][ld_in] (real_input != 0) or complex; out complex [B][ld_out].
+ * ------------------------------------------------------------------------- */
+int dsp_dft_size(int64_t n);
+int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_input,
+                int64_t ld_in, int64_t ld_out, const float* chirp, const float* chirp_fft,
+                const float* twiddles_m, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Windowed magnitude spectrum of one segment per row.

@@ -207,6 +207,26 @@ def test_fft_large_and_batched(gpu):
         assert np.max(np.abs(X - ref)) <= FFT_RTOL * np.max(np.abs(ref))
 
 
+def test_any_length_dft_matches_numpy(gpu):
+    """The app-side transform (app.py:322-324: np.fft.fft of int(1024*L/M)-sample
+    segments) for any length: max|dX| <= 1e-5 * max|X| against np.fft.fft,
+    real and complex rows, batched; powers of two go to the radix-2 kernel."""
+    rng = np.random.default_rng(21)
+    for n in (1, 2, 3, 5, 7, 100, 1000, 1114, 1536, 2047, 4096, 8191):
+        for real in (True, False):
+            x = rng.uniform(-1, 1, (3, n))
+            if not real:
+                x = x + 1j * rng.uniform(-1, 1, (3, n))
+            xt = torch.from_numpy(x.astype(np.float32 if real else np.complex64)).to(gpu)
+            got = _ops().dft(xt).cpu().numpy()
+            ref = np.fft.fft(x.astype(np.float32 if real else np.complex64).astype(
+                np.complex128), axis=1)
+            err = np.max(np.abs(got - ref), axis=1)
+            assert np.all(err <= FFT_RTOL * np.max(np.abs(ref), axis=1)), (n, real, err)
+    with pytest.raises(ValueError):
+        _ops().dft(torch.zeros((1, 9000), device=gpu))
+
+
 def test_fft_rejects_non_power_of_two(gpu):
     with pytest.raises(ValueError):
         _dc().fft_diezmado_en_tiempo(np.ones(12))

@@ -190,3 +190,19 @@ def test_stft_plan_framing():
     assert design.stft_plan(72000, 2048).hop == 512
     with pytest.raises(ValueError):
         design.stft_plan(1000, 1000)
+
+
+def test_bluestein_tables_compute_the_dft():
+    """The any-length DFT identity with the host tables (float64), as the
+    kernel applies it: A = FFT(x w), D = FFT(conj(A Bf)), X = w conj(D)."""
+    from dspcore import _lib
+    rng = np.random.default_rng(2)
+    for n in (1, 3, 1114, 1536, 8192):
+        chirp, bf, M = design.bluestein_tables(n)
+        assert M == _lib.load().dsp_dft_size(n) and M >= 2 * n - 1 and M & (M - 1) == 0
+        x = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+        a = np.zeros(M, complex)
+        a[:n] = x * chirp
+        d = np.fft.fft(np.conj(np.fft.fft(a) * bf))
+        got = chirp * np.conj(d[:n])
+        assert np.max(np.abs(got - np.fft.fft(x))) <= 1e-12 * max(1.0, np.max(np.abs(got)))
