@@ -208,7 +208,8 @@ struct Tw {
 template <int LOG2N>
 struct Tw<LOG2N, 15> {};
 
-template <int LOG2N, int P>
+// TSTR: stride into the caller's table (2 when the table is for 2N points).
+template <int LOG2N, int P, int TSTR = 1>
 __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restrict__ table,
                                         int j0) {
   using PL = Plan<LOG2N>;
@@ -218,9 +219,9 @@ __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restri
 #pragma unroll
     for (int b = 0; b < PL::RMAX / R; ++b) {
       const int m = (j0 + b * PL::TPT) & (NS - 1);
-      tw.w[b] = table[m * (PL::N / (NS * R))];
+      tw.w[b] = table[m * (PL::N / (NS * R)) * TSTR];
     }
-    load_tw<LOG2N, P + 1>(tw.next, table, j0);
+    load_tw<LOG2N, P + 1, TSTR>(tw.next, table, j0);
   }
 }
 
@@ -305,6 +306,93 @@ __global__ __launch_bounds__(Plan<LOG2N>::NT) void k_fft(FftArgs a) {
     Tw<LOG2N, 0> tw;
     load_tw<LOG2N, 0>(tw, a.tw, j0);
     run_pass<LOG2N, 0>(io, lds + tl * PL::PADN, j0, tw);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Real-input magnitude spectrum (spectrum / STFT mode, N >= 32): the N real
+// samples are packed as N/2 complex z[n] = x[2n] + i x[2n+1] (window applied),
+// one N/2-point Stockham transform Z runs in LDS, and the split
+//   E = (Z[k] + conj Z[N/2-k]) / 2,  O = (Z[k] - conj Z[N/2-k]) / (2i)
+//   X[k] = E + W_N^k O,  X[N/2-k] = conj(E - W_N^k O)
+// gives |X[k]| for every k <= N/2 from one (k, N/2-k) pair per thread: half the
+// butterflies and half the LDS of the complex transform.
+// ---------------------------------------------------------------------------
+template <int NH>  // NH = N/2, the complex transform's size
+struct RealSpecIO {
+  static constexpr bool kLdsIn = false;
+  const FftArgs& a;
+  InRow ir;
+  float2* buf;
+  bool live;
+  __device__ __forceinline__ float2 load(int n) const {
+    if (!live) return make_float2(0.f, 0.f);
+    const int i = 2 * n;
+    const float s0 = (i < ir.valid) ? a.in[ir.base + i] : 0.f;
+    const float s1 = (i + 1 < ir.valid) ? a.in[ir.base + i + 1] : 0.f;
+    return make_float2(s0 * a.win[i], s1 * a.win[i + 1]);
+  }
+  __device__ __forceinline__ void store(int k, float2 v) const { buf[lpad(k)] = v; }
+};
+
+template <int LOG2N>  // LOG2N of the real length N
+__global__ __launch_bounds__(Plan<LOG2N - 1>::NT) void k_spec_real(FftArgs a) {
+  using PL = Plan<LOG2N - 1>;
+  constexpr int N = 1 << LOG2N, NH = N / 2;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int tl = threadIdx.x / PL::TPT;
+  const int j0 = threadIdx.x - tl * PL::TPT;
+  const int64_t t = (int64_t)blockIdx.x * PL::TPB + tl;
+  const bool live = t < a.B;
+  float2* buf = lds + tl * PL::PADN;
+  Tw<LOG2N - 1, 0> tw;
+  load_tw<LOG2N - 1, 0, 2>(tw, a.tw, j0);
+  run_pass<LOG2N - 1, 0>(RealSpecIO<NH>{a, in_row<kSpec>(a, live ? t : 0), buf, live}, buf, j0,
+                         tw);
+  __syncthreads();  // the last pass stored Z into LDS
+  if (!live) return;
+  float* mr = a.out + t * a.ld_out;
+  for (int k = j0; k <= NH / 2; k += PL::TPT) {
+    const float2 zk = buf[lpad(k)];
+    const float2 zm = buf[lpad((NH - k) & (NH - 1))];
+    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+    const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+    const float2 w = a.tw[k < NH ? k : 0];  // k = NH/2 < N/2 always; table holds W_N^k, k < N/2
+    const float2 wo = cmul(o, w);
+    const float2 xk = cadd(e, wo), xm = csub(e, wo);
+    mr[k] = sqrtf(fmaf(xk.x, xk.x, xk.y * xk.y));
+    if (k > 0 && k < NH / 2) mr[NH - k] = sqrtf(fmaf(xm.x, xm.x, xm.y * xm.y));
+    if (k == 0) mr[NH] = fabsf(zk.x - zk.y);
+  }
+}
+
+template <int LOG2N>
+int launch_spec_real(const FftArgs& a, hipStream_t s) {
+  using PL = Plan<LOG2N - 1>;
+  const size_t shm = (size_t)PL::TPB * PL::PADN * sizeof(float2);
+  if (int rc = allow_lds(k_spec_real<LOG2N>, shm)) return rc;
+  const unsigned grid = (unsigned)ceil_div(a.B, PL::TPB);
+  hipLaunchKernelGGL(k_spec_real<LOG2N>, dim3(grid), dim3(PL::NT), shm, s, a);
+  DSP_LAUNCHED("k_spec_real");
+  return DSP_OK;
+}
+
+template <int MODE>
+int dispatch(const FftArgs& a, int log2n, hipStream_t s);
+
+int dispatch_spec(const FftArgs& a, int log2n, hipStream_t s) {
+  switch (log2n) {
+    case 5: return launch_spec_real<5>(a, s);
+    case 6: return launch_spec_real<6>(a, s);
+    case 7: return launch_spec_real<7>(a, s);
+    case 8: return launch_spec_real<8>(a, s);
+    case 9: return launch_spec_real<9>(a, s);
+    case 10: return launch_spec_real<10>(a, s);
+    case 11: return launch_spec_real<11>(a, s);
+    case 12: return launch_spec_real<12>(a, s);
+    case 13: return launch_spec_real<13>(a, s);
+    case 14: return launch_spec_real<14>(a, s);
+    default: return dispatch<kSpec>(a, log2n, s);
   }
 }
 
@@ -451,7 +539,7 @@ int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg
   FftArgs a{x, mag, B * frames, ld_x, ld_mag, seg_start, seg_len, hop, frames, window,
             reinterpret_cast<const float2*>(tw)};
   TraceScope trace(frames == 1 ? "spectrum" : "stft", s);
-  return dispatch<kSpec>(a, log2n, s);
+  return dispatch_spec(a, log2n, s);
 }
 
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
