@@ -29,10 +29,11 @@
 //           - or (chain) with G composed with the SRC taps, over the SRC input;
 //   scan:   S_0 = 0, S_{c+1} = A^T S_c + E_c  (A^T is computed on the host);
 //   pass 2: rerun every chunk from S_c, clip, store.
-// With C <= 64 and S <= 8 all three run in ONE kernel (k_iir_wave): one
-// wavefront owns one channel, lane c = chunk c, so tile staging, the carry scan
-// and both passes are wave-private -- no workgroup barrier anywhere, and each
-// wave streams independently of the others on its SIMD.  Otherwise the general
+// With C <= 256 and S <= 8 all three run in ONE kernel (k_iir_wave).  With
+// C <= 64 one wavefront owns one channel, lane c = chunk c, so tile staging, the
+// carry scan and both passes are wave-private -- no workgroup barrier anywhere,
+// and each wave streams independently of the others on its SIMD; up to 256
+// chunks use four such waves per channel and a block-wide scan.  Otherwise the general
 // path runs pass 1, a carry kernel and pass 2 as separate launches.  The
 // chunking depends only on the caller's chunk_len, never on B, so a row's
 // result is bitwise identical however the batch is sized or sharded.
@@ -96,7 +97,7 @@ constexpr int kNT = 256;       // lanes (rows) per block, general path
 constexpr int kTS = 32;        // samples per tile step (chunk_len granule)
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
 constexpr int kLoads = kTS / 4;  // float4 loads per thread per tile (one row per thread)
-constexpr int kCBMax = kWave;  // max chunks per channel in the fused kernel
+constexpr int kCBMax = 4 * kWave;  // max chunks per channel in the fused kernel
 #ifndef DSP_IIR_EXPERIMENT
 #define DSP_IIR_EXPERIMENT 0  // 1: no arithmetic, 2: no global loads (timing only)
 #endif
@@ -331,19 +332,31 @@ struct XState {
 // Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
 constexpr int kWaveTileFloats = kWave * kRow;
 
-template <int S, int P1, int VM, bool NORM>
-__global__ __launch_bounds__(kWave) void k_iir_wave(
+// W waves per channel (chunk c = 64*wave + lane, C <= 64*W).  W == 1: the
+// scan is wave-synchronous and the kernel has no workgroup barrier.  W > 1
+// (small batches: more chunks so that B*W waves still fill the chip): four
+// barriers around a block-wide serial scan run by wave 0.
+template <int W>
+__device__ __forceinline__ void block_sync() {
+  if constexpr (W == 1) asm volatile("" ::: "memory");
+  else __syncthreads();
+}
+
+template <int S, int P1, int VM, bool NORM, int W>
+__global__ __launch_bounds__(kWave * W) void k_iir_wave(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
     int64_t ld_x, int64_t ld_y, SosParams p, ScanParams sp,
     const double* __restrict__ G, int64_t T, int C, int clip, XState XS) {
   constexpr int D = 2 * S;
-  static_assert(kWave * D * 2 <= kWaveTileFloats, "scan must fit in the tile");
-  __shared__ __attribute__((aligned(16))) float tile[kWaveTileFloats];
-  __shared__ int64_t s_in[kWave], s_out[kWave];
-  __shared__ int s_len[kWave], s_lo[kWave];
-  double* scan = reinterpret_cast<double*>(tile);
+  static_assert(kWave * D * 2 <= kWaveTileFloats, "scan must fit in the tiles");
+  __shared__ __attribute__((aligned(16))) float tiles[W * kWaveTileFloats];
+  __shared__ int64_t s_in[kWave * W], s_out[kWave * W];
+  __shared__ int s_len[kWave * W], s_lo[kWave * W];
+  double* scan = reinterpret_cast<double*>(tiles);
 
   const int c = threadIdx.x;  // chunk
+  const int lane = c & (kWave - 1), wv = c / kWave;
+  float* tile = tiles + wv * kWaveTileFloats;
   const int64_t b = blockIdx.x;
   const bool live = c < C;
   const int64_t t_begin = (int64_t)c * T;
@@ -363,7 +376,8 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
   }
   // VM > 0 stores through a raw buffer based at this channel's output row.
   s_out[c] = live ? (VM > 0 ? 0 : b * ld_y) + t_begin : 0;
-  const Rows rows{s_in, s_out, s_len, s_lo};
+  const int r0 = wv * kWave;  // this wave's rows
+  const Rows rows{s_in + r0, s_out + r0, s_len + r0, s_lo + r0};
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(y + b * ld_y, 0, (int)(n * 4), 0x00020000);
 
@@ -375,14 +389,14 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   if constexpr (P1 == 2) {
-    run_pass<S, kStateTable, kWave, VM, true, NORM>(XS.xs, y, rsrc, tile, rows, XS.rows, c, s1, s2,
-                                               e, p, G, clip);
+    run_pass<S, kStateTable, kWave, VM, true, NORM>(XS.xs, y, rsrc, tile, rows, XS.rows, lane,
+                                                    s1, s2, e, p, G, clip);
   } else if constexpr (P1 == 1) {
-    run_pass<S, kStateTable, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p,
-                                                   G, clip);
+    run_pass<S, kStateTable, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1, s2,
+                                                        e, p, G, clip);
   } else {
-    run_pass<S, kStateCascade, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e,
-                                                     p, G, clip);
+    run_pass<S, kStateCascade, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1,
+                                                          s2, e, p, G, clip);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       e[2 * k] = s1[k];
@@ -392,8 +406,9 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
 
   // ---- carry scan: slot c holds E_c; step cc overwrites slot cc with
   // S_{cc+1} = P S_cc + E_cc (S_cc sits in slot cc-1), so chunk c >= 1 finds
-  // its initial state in slot c-1.  Lanes 0..D-1 each own one state
-  // component; the wave's LDS instructions execute in order.
+  // its initial state in slot c-1.  Lanes 0..D-1 of wave 0 each own one state
+  // component; a wave's LDS instructions execute in order.
+  block_sync<W>();  // W > 1: the scan slots overlap other waves' tiles
 #pragma unroll
   for (int i = 0; i < D; ++i) scan[c * D + i] = e[i];
   s_in[c] = in2;  // pass-2 rows; pass 2 opens with a hand-off
@@ -405,19 +420,22 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
 #pragma unroll
     for (int j = 0; j < D; ++j) prow[j] = sp.P[c * D + j];
   }
-  asm volatile("" ::: "memory");
-  for (int cc = 0; cc + 1 < C; ++cc) {
-    if (row_lane) {
-      double acc = scan[cc * D + c];
-      if (cc > 0) {
+  block_sync<W>();
+  if (wv == 0) {
+    for (int cc = 0; cc + 1 < C; ++cc) {
+      if (row_lane) {
+        double acc = scan[cc * D + c];
+        if (cc > 0) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) acc = fma(prow[j], scan[(cc - 1) * D + j], acc);
+          for (int j = 0; j < D; ++j) acc = fma(prow[j], scan[(cc - 1) * D + j], acc);
+        }
+        asm volatile("" ::: "memory");  // all reads of S_cc precede the write
+        scan[cc * D + c] = acc;
       }
-      asm volatile("" ::: "memory");  // all reads of S_cc precede the write
-      scan[cc * D + c] = acc;
+      asm volatile("" ::: "memory");
     }
-    asm volatile("" ::: "memory");
   }
+  block_sync<W>();
   if (c > 0) {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -428,11 +446,11 @@ __global__ __launch_bounds__(kWave) void k_iir_wave(
 #pragma unroll
     for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
   }
-  asm volatile("" ::: "memory");
+  block_sync<W>();  // W > 1: states read before the tiles are reused
 
   // ---- pass 2: outputs from the carried state
-  run_pass<S, kApply, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, c, s1, s2, e, p, G,
-                                            clip);
+  run_pass<S, kApply, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1, s2, e, p,
+                                                 G, clip);
 }
 
 // ---------------------------------------------------------------------------
@@ -662,9 +680,16 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const bool span_ok = n * 4 < (int64_t)kOob;
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
   const dim3 grid((unsigned)B);
-#define DSP_WAVE_LAUNCH(P1v, VMv, NV)                                                       \
-  hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV>), grid, dim3(kWave), 0, s, x, y, B, n,     \
-                     ld_x, ld_y, p, sp, G, T, C, clip, XS)
+  const int W = C <= kWave ? 1 : 4;
+#define DSP_WAVE_LAUNCH(P1v, VMv, NV)                                                         \
+  do {                                                                                        \
+    if (W == 1)                                                                               \
+      hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV, 1>), grid, dim3(kWave), 0, s, x, y, B,  \
+                         n, ld_x, ld_y, p, sp, G, T, C, clip, XS);                            \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV, 4>), grid, dim3(4 * kWave), 0, s, x, y, \
+                         B, n, ld_x, ld_y, p, sp, G, T, C, clip, XS);                         \
+  } while (0)
 #define DSP_WAVE_VM(P1v, NV)                         \
   if (VMr == 1) DSP_WAVE_LAUNCH(P1v, 1, NV);         \
   else if (VMr == 2) DSP_WAVE_LAUNCH(P1v, 2, NV);    \

@@ -12,8 +12,8 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, spectrum_plan,
-                     src_plan, xstate_chunk_len)
+from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, max_chunks_for,
+                     spectrum_plan, src_plan, xstate_chunk_len)
 
 
 @dataclass(frozen=True)
@@ -52,15 +52,18 @@ class Chain:
         # x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
         # the row into far fewer chunks than the plain rule.
-        plain = chunk_len_for(n_out)
-        xs_len = xstate_chunk_len(n_out, cfg.L, cfg.M)
-        self.xstate = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
-                       and 1 <= S <= 8 and S != 7 and xs_len <= 2 * plain
-                       and (chunk_len is None or int(chunk_len) == xs_len))
+        mc = max_chunks_for(self.B)
+        plain = chunk_len_for(n_out, mc)
+        eligible = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
+                    and 1 <= S <= 8 and S != 7)
         if chunk_len is not None:
-            self.chunk_len = int(chunk_len)
+            T = int(chunk_len)
+            self.xstate = eligible and T % 32 == 0 and (T * cfg.M) % (4 * cfg.L) == 0
         else:
-            self.chunk_len = xs_len if self.xstate else plain
+            xs_len = xstate_chunk_len(n_out, cfg.L, cfg.M, mc)
+            self.xstate = eligible and xs_len <= 2 * plain
+            T = xs_len if self.xstate else plain
+        self.chunk_len = T
         dev = self.device
         self.taps = ops.taps_tensor(self.src, dev)
         self.window = ops._table("hann", self.spec.n_fft, dev)

@@ -156,11 +156,25 @@ def tf_to_sos_row(b, a) -> np.ndarray:
     return np.array([bb[0], bb[1], bb[2], aa[1], aa[2]])
 
 
-def chunk_len_for(n: int, max_chunks: int = 64) -> int:
+MAX_FUSED_CHUNKS = 256   # csrc/iir.hip kCBMax: four waves of 64 chunk lanes per channel
+WIDE_BATCH = 2048        # from this many channels one wave (<= 64 chunks) per channel fills the chip
+
+
+def max_chunks_for(batch: int) -> int:
+    """Chunks per channel the cascade plans for a batch of `batch` channels:
+    <= 64 (one wavefront per channel, no barriers) once the batch alone fills
+    the chip with waves, else <= 256 (four wavefronts per channel) so that small
+    batches still do.  Rows are bitwise independent of the batch size for a
+    given chunk length; across this threshold they agree to rounding."""
+    return 64 if int(batch) >= WIDE_BATCH else MAX_FUSED_CHUNKS
+
+
+def chunk_len_for(n: int, max_chunks: int = MAX_FUSED_CHUNKS) -> int:
     """Chunk length of the biquad carry scan for a row of n samples: the
     smallest multiple of 32 that splits the row into <= max_chunks chunks, so the
-    cascade runs as one fused launch (include/dspcore.h).  A function of n
-    only: every row's result is independent of the batch size."""
+    cascade runs as one fused launch (include/dspcore.h) with enough chunk lanes
+    to fill the chip at small batches.  A function of n only: every row's
+    result is independent of the batch size."""
     per = -(-int(n) // max_chunks)
     return max(32, -(-per // 32) * 32)
 
@@ -228,7 +242,7 @@ def state_response_table(sos: np.ndarray, chunk_len: int) -> np.ndarray:
     return np.ascontiguousarray(G[::-1])
 
 
-def xstate_chunk_len(n_out: int, L: int, M: int, max_chunks: int = 64) -> int:
+def xstate_chunk_len(n_out: int, L: int, M: int, max_chunks: int = MAX_FUSED_CHUNKS) -> int:
     """Chunk length for the chain's x-domain chunk states (include/dspcore.h,
     dsp_chain_f32): the smallest multiple of 32 with chunk_len*M/L an integer
     multiple of 32 (128-byte aligned x rows) that splits n_out into between

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .design import SrcPlan, chunk_len_for, hann, state_response_table, twiddles
+from .design import SrcPlan, chunk_len_for, hann, max_chunks_for, state_response_table, twiddles
 from .design import xstate_table as xstate_table_host
 
 _tables_lock = threading.Lock()
@@ -97,7 +97,7 @@ def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = No
 
 def biquad_workspace(B: int, n: int, S: int, device: torch.device,
                      chunk_len: int | None = None) -> torch.Tensor:
-    chunk_len = chunk_len_for(n) if chunk_len is None else chunk_len
+    chunk_len = chunk_len_for(n, max_chunks_for(B)) if chunk_len is None else chunk_len
     nbytes = _lib.load().dsp_biquad_workspace_bytes(B, n, S, chunk_len)
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
@@ -162,7 +162,7 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     sos = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 5)
     B, n = x.shape
     S = sos.shape[0]
-    chunk_len = chunk_len_for(n) if chunk_len is None else int(chunk_len)
+    chunk_len = chunk_len_for(n, max_chunks_for(B)) if chunk_len is None else int(chunk_len)
     if out is None:
         out = torch.empty_like(x)
     if workspace is None:

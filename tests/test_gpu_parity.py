@@ -135,9 +135,11 @@ def test_eq_chunk_carry_is_exact_to_rounding(gpu):
                                  "High Mids": -12, "Presence": 9, "Brilliance": -9}).sos
     z_one = ops.biquad_cascade(x, sos, True, chunk_len=72000 + 32 - 72000 % 32).cpu().numpy()
     variants = {
-        "fused+table": dict(),
-        "fused": dict(use_table=False),
+        "fused+table (4 waves, 250 chunks)": dict(),
+        "fused (4 waves, 250 chunks)": dict(use_table=False),
+        "fused+table, 1 wave, 63 chunks": dict(chunk_len=1152),
         "fused, 36 chunks": dict(chunk_len=2048),
+        "fused 4 waves, 141 chunks": dict(chunk_len=512),
         "general, 282 chunks": dict(chunk_len=256),
     }
     for name, kw in variants.items():
@@ -325,7 +327,7 @@ def test_chain_config3_full_batch(gpu):
     torch.cuda.synchronize()
     assert torch.isfinite(z).all() and torch.isfinite(mag).all()
     assert float(z.abs().max()) <= 1.0
-    one = Chain(cfg, 1, gpu)
+    one = Chain(cfg, 1, gpu, chunk_len=ch.chunk_len)   # same chunking: bitwise rows
     for b in (0, 1234, B - 1):
         xb = x[b].cpu().numpy()
         ry, rz, _, rmag, _ = orc.chain(xb.astype(np.float32), 48000, 3, 2, orc.CONFIG3_GAINS,

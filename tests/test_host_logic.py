@@ -145,8 +145,8 @@ def test_chunk_policy_is_batch_independent_and_fused():
     for n in (1, 31, 32, 100, 4800, 72000, 52245, 10 ** 6):
         T = design.chunk_len_for(n)
         assert T % 32 == 0 and T >= 32
-        assert -(-n // T) <= 64
-    assert design.chunk_len_for(72000) == 1152
+        assert -(-n // T) <= design.MAX_FUSED_CHUNKS
+    assert design.chunk_len_for(72000) == 288 and design.chunk_len_for(72000, 64) == 1152
 
 
 def test_xstate_table_reproduces_output_domain_states():
@@ -164,7 +164,7 @@ def test_xstate_table_reproduces_output_domain_states():
         plan = design.src_plan(n_in, fs, M, L, K)
         sos = design.eq_plan(plan.fs_out, gains).sos
         T = design.xstate_chunk_len(plan.n_out, L, M)
-        assert T % 32 == 0 and (T * M) % (4 * L) == 0 and -(-plan.n_out // T) <= 64
+        assert T % 32 == 0 and (T * M) % (4 * L) == 0 and -(-plan.n_out // T) <= 256
         out = [ctypes.c_int64() for _ in range(3)]
         assert lib.dsp_chain_xstate_geometry(T, plan.K, L, M, plan.c_offset,
                                              *[ctypes.byref(o) for o in out]) == 0

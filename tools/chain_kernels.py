@@ -18,7 +18,13 @@ cfg = ChainConfig(48000, 48000, 3, 2, None, gains, n_fft=4096)
 dev = torch.device("cuda", 0)
 x = torch.rand((B, 48000), device=dev, generator=torch.Generator(device=dev).manual_seed(0))
 x = x * 2 - 1
-variants = {"xstate": dict(), "ytable": dict(use_xstate=False)}
+variants = {"xstate": dict(), "ytable": dict(use_xstate=False),
+            "xstate1152": dict(chunk_len=1152), "ytable1152": dict(use_xstate=False, chunk_len=1152)}
+if os.environ.get("CHAIN_C5"):
+    B = int(os.environ.get("CHAIN_B", 1024))
+    cfg = ChainConfig(48000, 44100, 160, 147, 1023, gains, n_fft=4096)
+    x = torch.rand((B, 48000), device=dev) * 2 - 1
+    variants = {"c5": dict(), "c5_T1280": dict(chunk_len=1280)}
 res = {}
 for name, kw in variants.items():
     ch = Chain(cfg, B, dev, **kw)
