@@ -130,7 +130,7 @@ __global__ __launch_bounds__(NT) void k_src_reg(
 // LDS: tap bank [L][T] + input window, both carved from dynamic LDS.
 // ---------------------------------------------------------------------------
 constexpr int kGenNT = 256;
-constexpr int kGenTile = 1024;
+constexpr int kGenTile = 4096;
 
 __global__ __launch_bounds__(kGenNT) void k_src_generic(
     const float* __restrict__ x, float* __restrict__ y, int64_t n_in,
@@ -159,11 +159,16 @@ __global__ __launch_bounds__(kGenNT) void k_src_generic(
   __syncthreads();
 
   // Output stores are coalesced directly (consecutive threads, consecutive m).
+  // (q, phi) of j = m*M + c advance by a fixed (dq, dphi) per iteration, so the
+  // 64-bit division happens once per thread.
   (void)vec_y;
+  const int64_t j0 = (m0 + tid) * M + c;
+  int64_t q = j0 / L;
+  int phi = (int)(j0 - q * L);
+  const int64_t step = (int64_t)kGenNT * M;
+  const int64_t dq = step / L;
+  const int dphi = (int)(step - dq * L);
   for (int64_t m = m0 + tid; m < m1; m += kGenNT) {
-    const int64_t j = m * M + c;
-    const int64_t q = j / L;
-    const int phi = (int)(j - q * L);
     const float* w = s_win + (int)(q - (T - 1) - qa);
     const float* h = s_bank + phi * T;
     float a0 = 0.f, a1 = 0.f;
@@ -174,6 +179,12 @@ __global__ __launch_bounds__(kGenNT) void k_src_generic(
     }
     if (u < T) a0 = fmaf(h[u], w[u], a0);
     yr[m] = a0 + a1;
+    q += dq;
+    phi += dphi;
+    if (phi >= L) {
+      phi -= L;
+      ++q;
+    }
   }
 }
 
