@@ -141,6 +141,7 @@ def kernel_bytes(chain, name):
         "iir_xstate": 8 * B * n_out,
         "iir_prep": 8 * (2 * S) ** 2,
         "spectrum": 4 * B * (chain.spec.seg_len + N // 2 + 1),
+        "stft": 0,
     }.get(name, 0)
 
 
