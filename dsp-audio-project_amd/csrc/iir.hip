@@ -44,6 +44,7 @@
 // into registers before the current tile is computed, so HBM latency hides
 // under the fp64 work.  Pass 2 writes its outputs back into the tile and stores
 // it with the same coalesced pattern.
+#include <climits>
 #include <cmath>
 #include <vector>
 
@@ -119,11 +120,13 @@ __device__ __forceinline__ double cascade_step(double u, double (&w1)[S > 0 ? S 
   return u;
 }
 
-__device__ __forceinline__ float clip1(float v) {
-  // np.clip semantics: NaN stays NaN.  Clipping after the float32 rounding
-  // gives the same result as rounding the float64 clip (|v| <= 1 rounds to
-  // |v| <= 1, and anything beyond rounds to beyond-or-equal).
-  return v < -1.f ? -1.f : (v > 1.f ? 1.f : v);
+// np.clip(v, lo, hi) with NaN kept (v_med3_f32 maps NaN to a bound).
+// Clipping after the float32 rounding gives the same result as rounding the
+// float64 clip (|v| <= 1 rounds to |v| <= 1, anything beyond rounds to
+// beyond-or-equal).  lo/hi = -inf/+inf is the identity.
+__device__ __forceinline__ float clip_f32(float v, float lo, float hi) {
+  const float m = __builtin_amdgcn_fmed3f(v, lo, hi);
+  return v != v ? v : m;
 }
 
 // Row descriptors live in LDS: global offset of the row's first sample for
@@ -159,13 +162,13 @@ __device__ __forceinline__ void tile_sync() {
 // their use.  !VEC: guarded scalar loads (slow path for odd pitches).
 template <int NR, bool VEC>
 __device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restrict__ x,
-                                      const Rows& rows, int64_t t0, int tid) {
+                                      const Rows& rows, int t0, int tid) {
   const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
     const int r = i * (NR / 8) + (tid >> 3);
     const int len = rows.len[r];
-    const int64_t t = t0 + c4;
+    const int t = t0 + c4;
     if constexpr (VEC) {
       const float* src = (t < len && t >= rows.lo[r]) ? x + rows.in[r] + t : x;
       v[i] = *reinterpret_cast<const float4*>(src);
@@ -180,21 +183,30 @@ __device__ __forceinline__ void fetch(float4 (&v)[kLoads], const float* __restri
   }
 }
 
-// Writes the fetched tile into LDS, zeroing samples outside each row's range.
-template <int NR>
+// Writes the fetched tile into LDS; MASK: zeroes samples outside each row's
+// range (one unsigned compare per sample: t - lo < len - lo).
+template <int NR, bool MASK>
 __device__ __forceinline__ void tile_put(float* tile, const float4 (&v)[kLoads],
-                                         const Rows& rows, int64_t t0, int tid) {
+                                         const Rows& rows, int t0, int tid) {
   const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
     const int r = i * (NR / 8) + (tid >> 3);
-    const int64_t t = t0 + c4;
-    const int len = rows.len[r], lo = rows.lo[r];
     float* d = tile + r * kRow + c4;
-    d[0] = (t + 0 < len && t + 0 >= lo) ? v[i].x : 0.f;
-    d[1] = (t + 1 < len && t + 1 >= lo) ? v[i].y : 0.f;
-    d[2] = (t + 2 < len && t + 2 >= lo) ? v[i].z : 0.f;
-    d[3] = (t + 3 < len && t + 3 >= lo) ? v[i].w : 0.f;
+    if constexpr (MASK) {
+      const int lo = rows.lo[r];
+      const int len = rows.len[r];
+      const uint32_t a = (uint32_t)(t0 + c4 - lo), w = len > lo ? (uint32_t)(len - lo) : 0u;
+      d[0] = a + 0 < w ? v[i].x : 0.f;
+      d[1] = a + 1 < w ? v[i].y : 0.f;
+      d[2] = a + 2 < w ? v[i].z : 0.f;
+      d[3] = a + 3 < w ? v[i].w : 0.f;
+    } else {
+      d[0] = v[i].x;
+      d[1] = v[i].y;
+      d[2] = v[i].z;
+      d[3] = v[i].w;
+    }
   }
 }
 
@@ -210,14 +222,14 @@ constexpr uint32_t kOob = 0x80000000u;  // > any buffer span (checked on host)
 
 template <int NR, int SM>
 __device__ __forceinline__ void tile_store(float* __restrict__ y, __amdgpu_buffer_rsrc_t rsrc,
-                                           const float* tile, const Rows& rows, int64_t t0,
+                                           const float* tile, const Rows& rows, int t0,
                                            int tid) {
   const int c4 = (tid & 7) * 4;
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) {
     const int r = i * (NR / 8) + (tid >> 3);
     const int len = rows.len[r];
-    const int64_t t = t0 + c4;
+    const int t = t0 + c4;
     const float* s = tile + r * kRow + c4;
     if constexpr (SM == 0) {
       float* dst = y + rows.out[r] + t;
@@ -248,16 +260,76 @@ __device__ __forceinline__ void tile_store(float* __restrict__ y, __amdgpu_buffe
   }
 }
 
+// Affine row addressing for the one-channel-per-wave kernel (VM > 0): row r of
+// a pass starts at byte r*stride*4 + start*4 of one channel's row, so vector i
+// of a thread sits at base + i*step + t0*4 with base/step fixed for the pass.
+// Loads and stores go through raw buffers spanning that channel's row only:
+// offsets past the end (or "negative", i.e. >= 2^31) read zeros and drop
+// stores in hardware, so neither needs a per-vector guard or a row descriptor.
+struct AffIO {
+  __amdgpu_buffer_rsrc_t in;
+  int in_base, in_step;    // bytes
+  int out_base, out_step;  // bytes, into the y buffer resource
+};
+
+__device__ __forceinline__ AffIO aff_rows(__amdgpu_buffer_rsrc_t in, int64_t in_stride,
+                                          int64_t in_start, int64_t out_stride, int first_row,
+                                          int tid) {
+  const int r = first_row + (tid >> 3), c4 = (tid & 7) * 4;
+  AffIO io;
+  io.in = in;
+  io.in_base = (int)(((int64_t)r * in_stride + in_start + c4) * 4);
+  io.in_step = (int)(in_stride * 4 * (kWave / 8));
+  io.out_base = (int)(((int64_t)r * out_stride + c4) * 4);
+  io.out_step = (int)(out_stride * 4 * (kWave / 8));
+  return io;
+}
+
+__device__ __forceinline__ void fetch_aff(float4 (&v)[kLoads], const AffIO& io, int t0) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    const f32x4 a = __builtin_amdgcn_raw_buffer_load_b128(io.in, io.in_base + i * io.in_step + t0 * 4,
+                                                          0, 0);
+    v[i] = make_float4(a.x, a.y, a.z, a.w);
+  }
+}
+
+template <int SM>
+__device__ __forceinline__ void store_aff(__amdgpu_buffer_rsrc_t rsrc, const float* tile,
+                                          const AffIO& io, int t0, int tid) {
+  const int c4 = (tid & 7) * 4;
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    const int r = i * (kWave / 8) + (tid >> 3);
+    const float* s = tile + r * kRow + c4;
+    const int off = io.out_base + i * io.out_step + t0 * 4;
+    if constexpr (SM == 1) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 d;
+      d.x = __float_as_uint(s[0]);
+      d.y = __float_as_uint(s[1]);
+      d.z = __float_as_uint(s[2]);
+      d.w = __float_as_uint(s[3]);
+      __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, off, 0, 0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s[e]), rsrc, off + 4 * e, 0, 0);
+    }
+  }
+}
+
 enum PassMode { kStateCascade = 0, kStateTable = 1, kApply = 2 };
 
 // One pass over every row of the NR-row group, tile by tile, with the next
 // tile's loads in flight during the current tile's arithmetic.  Samples outside
 // a row's range are zeros; their outputs are never stored.  Starts with a
 // hand-off (fetch reads other threads' row descriptors) and ends with one.
-template <int S, int MODE, int NR, int VM, bool VIN, bool NORM>
+template <int S, int MODE, int NR, int VM, bool VIN, bool NORM, bool AFF = false>
 __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __restrict__ y,
                                          __amdgpu_buffer_rsrc_t rsrc, float* tile,
-                                         const Rows& rows, int64_t T, int tid,
+                                         const Rows& rows, const AffIO& io, int64_t T, int tid,
                                          double (&s1)[S > 0 ? S : 1],
                                          double (&s2)[S > 0 ? S : 1],
                                          double (&e)[S > 0 ? 2 * S : 1], const SosParams& p,
@@ -270,14 +342,38 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 #pragma unroll
   for (int i = 0; i < kLoads; ++i) v[i] = make_float4(0.25f, -0.5f, 0.125f, 0.75f);
 #else
-  fetch<NR, VIN>(v, x, rows, 0, tid);
+  if constexpr (AFF) fetch_aff(v, io, 0);
+  else fetch<NR, VIN>(v, x, rows, 0, tid);
 #endif
-  for (int64_t t0 = 0; t0 < T; t0 += kTS) {
+  // Tiles in [span_lo, span_hi) lie inside the range of every row of the wave
+  // that has one and are put unmasked (a row without samples is a chunk whose
+  // state is never used).  Pass 2 never masks: outputs past a row's end are
+  // not stored.
+  int span_lo = 0, span_hi = MODE == kApply ? INT_MAX : 0;
+  if constexpr (NR == kWave && MODE != kApply) {
+    const int len = rows.len[tid], lo = rows.lo[tid];
+    int a = len > 0 ? lo : 0, z = len > 0 ? len : INT_MAX;
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+      a = max(a, __shfl_xor(a, m));
+      z = min(z, __shfl_xor(z, m));
+    }
+    span_lo = __builtin_amdgcn_readfirstlane(a);
+    span_hi = __builtin_amdgcn_readfirstlane(z);
+  }
+  const float clo = clip ? -1.f : -INFINITY, chi = clip ? 1.f : INFINITY;
+  for (int t0 = 0; t0 < (int)T; t0 += kTS) {
     tile_sync<NR>();  // readers of the previous tile are done
-    tile_put<NR>(tile, v, rows, t0, tid);
+    if (t0 >= span_lo && t0 + kTS <= span_hi)
+      tile_put<NR, false>(tile, v, rows, t0, tid);
+    else
+      tile_put<NR, true>(tile, v, rows, t0, tid);
     tile_sync<NR>();
 #if DSP_IIR_EXPERIMENT != 2 && DSP_IIR_EXPERIMENT != 4
-    if (t0 + kTS < T) fetch<NR, VIN>(v, x, rows, t0 + kTS, tid);
+    if (t0 + kTS < (int)T) {
+      if constexpr (AFF) fetch_aff(v, io, t0 + kTS);
+      else fetch<NR, VIN>(v, x, rows, t0 + kTS, tid);
+    }
 #endif
 #if DSP_IIR_EXPERIMENT == 1
     if (MODE == kStateTable) e[0] += my[3];
@@ -298,7 +394,7 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 #pragma unroll 8
       for (int j = 0; j < kTS; ++j) {
         const float out = (float)cascade_step<S, NORM>((double)my[j], s1, s2, p);
-        if constexpr (MODE == kApply) my[j] = clip ? clip1(out) : out;
+        if constexpr (MODE == kApply) my[j] = clip_f32(out, clo, chi);
       }
     }
     if constexpr (MODE == kApply) {
@@ -306,7 +402,8 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 #if DSP_IIR_EXPERIMENT == 3 || DSP_IIR_EXPERIMENT == 4
       if (clip == 12345)
 #endif
-      tile_store<NR, VM>(y, rsrc, tile, rows, t0, tid);
+      if constexpr (AFF) store_aff<VM>(rsrc, tile, io, t0, tid);
+      else tile_store<NR, VM>(y, rsrc, tile, rows, t0, tid);
     }
   }
   tile_sync<NR>();
@@ -380,6 +477,21 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
   const Rows rows{s_in + r0, s_out + r0, s_len + r0, s_lo + r0};
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(y + b * ld_y, 0, (int)(n * 4), 0x00020000);
+  // VM > 0: affine buffer addressing (AffIO); loads may read up to the next
+  // multiple of 4 samples (inside the row pitch, as the vector fetch does).
+  AffIO io1{}, io2{};
+  if constexpr (VM > 0) {
+    const __amdgpu_buffer_rsrc_t in2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x) + b * ld_x, 0, (int)(((n + 3) & ~3) * 4), 0x00020000);
+    io2 = aff_rows(in2, T, 0, T, r0, lane);
+    if constexpr (P1 == 2) {
+      const __amdgpu_buffer_rsrc_t in1 = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(XS.xs) + b * XS.ld, 0, (int)(((XS.n + 3) & ~3) * 4), 0x00020000);
+      io1 = aff_rows(in1, XS.shift, XS.q0, T, r0, lane);
+    } else {
+      io1 = io2;
+    }
+  }
 
   double s1[S], s2[S], e[D];
 #pragma unroll
@@ -388,15 +500,16 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
   for (int i = 0; i < D; ++i) e[i] = 0.0;
 
   // ---- pass 1: zero-state end state of the lane's chunk
+  constexpr bool AFF = VM > 0;
   if constexpr (P1 == 2) {
-    run_pass<S, kStateTable, kWave, VM, true, NORM>(XS.xs, y, rsrc, tile, rows, XS.rows, lane,
-                                                    s1, s2, e, p, G, clip);
+    run_pass<S, kStateTable, kWave, VM, true, NORM, AFF>(XS.xs, y, rsrc, tile, rows, io1,
+                                                         XS.rows, lane, s1, s2, e, p, G, clip);
   } else if constexpr (P1 == 1) {
-    run_pass<S, kStateTable, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1, s2,
-                                                        e, p, G, clip);
+    run_pass<S, kStateTable, kWave, VM, (VM > 0), NORM, AFF>(x, y, rsrc, tile, rows, io1, T,
+                                                             lane, s1, s2, e, p, G, clip);
   } else {
-    run_pass<S, kStateCascade, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1,
-                                                          s2, e, p, G, clip);
+    run_pass<S, kStateCascade, kWave, VM, (VM > 0), NORM, AFF>(x, y, rsrc, tile, rows, io1, T,
+                                                               lane, s1, s2, e, p, G, clip);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       e[2 * k] = s1[k];
@@ -449,8 +562,8 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
   block_sync<W>();  // W > 1: states read before the tiles are reused
 
   // ---- pass 2: outputs from the carried state
-  run_pass<S, kApply, kWave, VM, (VM > 0), NORM>(x, y, rsrc, tile, rows, T, lane, s1, s2, e, p,
-                                                 G, clip);
+  run_pass<S, kApply, kWave, VM, (VM > 0), NORM, AFF>(x, y, rsrc, tile, rows, io2, T, lane, s1,
+                                                      s2, e, p, G, clip);
 }
 
 // ---------------------------------------------------------------------------
@@ -496,10 +609,12 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
   // Rows span many channels here: guarded loads and stores (VM 0).
   const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0, 0x00020000);
   if (vec_x)
-    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, true, NORM>(x, y, none, tile, rows, T, tid, s1,
-                                                              s2, e, p, nullptr, clip);
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, true, NORM>(x, y, none, tile, rows,
+                                                                    AffIO{}, T, tid, s1, s2, e,
+                                                                    p, nullptr, clip);
   else
-    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, false, NORM>(x, y, none, tile, rows, T, tid,
+    run_pass<S, APPLY ? kApply : kStateCascade, kNT, 0, false, NORM>(x, y, none, tile, rows,
+                                                                     AffIO{}, T, tid,
                                                                s1, s2, e, p, nullptr, clip);
   if (!APPLY && live) {
     double* eo = e_out + g * (2 * S);
@@ -677,7 +792,7 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
   // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
   // address one channel's row with a 31-bit byte offset.
-  const bool span_ok = n * 4 < (int64_t)kOob;
+  const bool span_ok = n * 4 + 16 < (int64_t)kOob && (p1mode != 2 || XS.n * 4 + 16 < (int64_t)kOob);
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
   const dim3 grid((unsigned)B);
   const int W = C <= kWave ? 1 : 4;
