@@ -139,6 +139,7 @@ def kernel_bytes(chain, name):
         "iir_apply": 8 * B * n_out + 8 * 2 * S * B * C,
         "iir_fused": 8 * B * n_out,
         "iir_xstate": 8 * B * n_out,
+        "chain_fused": 4 * B * n_in + 8 * B * n_out,   # x read, y and z written
         "iir_prep": 8 * (2 * S) ** 2,
         "spectrum": 4 * B * (chain.spec.seg_len + N // 2 + 1),
         "stft": 0,

@@ -22,6 +22,7 @@ struct TraceState {
   size_t used = 0;
 };
 thread_local TraceState g_trace;
+thread_local bool g_chain_fusion = false;  // measured slower
 }  // namespace
 
 TraceScope::TraceScope(const char* name, hipStream_t s) : slot_(-1), s_(s) {
@@ -128,6 +129,13 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_
                           window, twiddles, static_cast<hipStream_t>(stream));
 }
 
+int dsp_chain_fusion(int32_t mode) {
+  dsp::clear_error();
+  const int prev = dsp::g_chain_fusion ? 1 : 0;
+  if (mode >= 0) dsp::g_chain_fusion = mode != 0;
+  return prev;
+}
+
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
   return dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
 }
@@ -151,7 +159,15 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
   if (B == 0) return DSP_OK;
-  int rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
+  int rc = dsp::kNotFused;
+  if (xstate_table && S > 0 && dsp::g_chain_fusion)
+    rc = dsp::launch_chain_fused(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
+                                 sos_host, S, clip, chunk_len, xstate_table, xstate_rows, s);
+  if (rc == DSP_OK)
+    return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
+                                twiddles, s);
+  if (rc != dsp::kNotFused) return rc;
+  rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
   if (rc) return rc;
   if (xstate_table && S > 0)
     rc = dsp::launch_biquad_xstate(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len, x,

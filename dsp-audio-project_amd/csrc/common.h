@@ -109,6 +109,13 @@ int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, in
 // the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
                     int64_t* q0, int64_t* rows);
+// Fused SRC + cascade (one launch, y never re-read).  Returns kNotFused, with
+// nothing launched, when the geometry has no instantiation.
+constexpr int kNotFused = 1;
+int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
+                       int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
+                       int L, int M, int64_t c, const double* sos, int S, int clip,
+                       int64_t chunk_len, const double* gx, int64_t gx_rows, hipStream_t s);
 int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
                          int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
                          const float* xs, int64_t n_in, int64_t ld_xs, int K, int L, int M,

@@ -99,6 +99,10 @@ constexpr int kTS = 32;        // samples per tile step (chunk_len granule)
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
 constexpr int kLoads = kTS / 4;  // float4 loads per thread per tile (one row per thread)
 constexpr int kCBMax = 4 * kWave;  // max chunks per channel in the fused kernel
+#ifndef DSP_CHAIN_EXP
+#define DSP_CHAIN_EXP 0  // fused chain timing ablations: 1 no SRC FMAs, 2 no cascade, 3 no y/z stores,
+                         // 4/5 32 of NOUT outputs stored at 128-B aligned / NOUT-strided offsets
+#endif
 #ifndef DSP_IIR_EXPERIMENT
 #define DSP_IIR_EXPERIMENT 0  // 1: no arithmetic, 2: no global loads (timing only)
 #endif
@@ -439,6 +443,53 @@ __device__ __forceinline__ void block_sync() {
   else __syncthreads();
 }
 
+// Carry scan over the C chunks of one channel.  Slot c of `scan` ([C][2S]
+// doubles in LDS) receives E_c; step cc overwrites slot cc with
+// S_{cc+1} = P S_cc + E_cc (S_cc sits in slot cc-1), so chunk c >= 1 finds its
+// initial state in slot c-1.  Lanes 0..D-1 of wave 0 each own one state
+// component; a wave's LDS instructions execute in order.  c = thread index in
+// the block (chunk); leaves chunk c's initial state in s1/s2.
+template <int S, int W>
+__device__ __forceinline__ void carry_scan(double* scan, const double (&e)[2 * S],
+                                           double (&s1)[S], double (&s2)[S],
+                                           const ScanParams& sp, int c, int C) {
+  constexpr int D = 2 * S;
+#pragma unroll
+  for (int i = 0; i < D; ++i) scan[c * D + i] = e[i];
+  const bool row_lane = c < D;
+  double prow[D];
+  if (row_lane) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) prow[j] = sp.P[c * D + j];
+  }
+  block_sync<W>();
+  if (c < kWave) {
+    for (int cc = 0; cc + 1 < C; ++cc) {
+      if (row_lane) {
+        double acc = scan[cc * D + c];
+        if (cc > 0) {
+#pragma unroll
+          for (int j = 0; j < D; ++j) acc = fma(prow[j], scan[(cc - 1) * D + j], acc);
+        }
+        asm volatile("" ::: "memory");  // all reads of S_cc precede the write
+        scan[cc * D + c] = acc;
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+  block_sync<W>();
+  // Branch-free (a divergent branch here made the compiler select through a
+  // scratch slot, whose reload then forced vmcnt(0) waits inside pass 2).
+  const int src = c > 0 ? c - 1 : 0;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const double a1 = scan[src * D + 2 * k], a2 = scan[src * D + 2 * k + 1];
+    s1[k] = c > 0 ? a1 : 0.0;
+    s2[k] = c > 0 ? a2 : 0.0;
+  }
+  block_sync<W>();  // W > 1: states read before the tiles are reused
+}
+
 template <int S, int P1, int VM, bool NORM, int W>
 __global__ __launch_bounds__(kWave * W) void k_iir_wave(
     const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t n,
@@ -517,53 +568,220 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
     }
   }
 
-  // ---- carry scan: slot c holds E_c; step cc overwrites slot cc with
-  // S_{cc+1} = P S_cc + E_cc (S_cc sits in slot cc-1), so chunk c >= 1 finds
-  // its initial state in slot c-1.  Lanes 0..D-1 of wave 0 each own one state
-  // component; a wave's LDS instructions execute in order.
+  // ---- carry scan
   block_sync<W>();  // W > 1: the scan slots overlap other waves' tiles
-#pragma unroll
-  for (int i = 0; i < D; ++i) scan[c * D + i] = e[i];
   s_in[c] = in2;  // pass-2 rows; pass 2 opens with a hand-off
   s_lo[c] = 0;
   s_len[c] = len2;
-  const bool row_lane = c < D;
-  double prow[D];
-  if (row_lane) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) prow[j] = sp.P[c * D + j];
-  }
-  block_sync<W>();
-  if (wv == 0) {
-    for (int cc = 0; cc + 1 < C; ++cc) {
-      if (row_lane) {
-        double acc = scan[cc * D + c];
-        if (cc > 0) {
-#pragma unroll
-          for (int j = 0; j < D; ++j) acc = fma(prow[j], scan[(cc - 1) * D + j], acc);
-        }
-        asm volatile("" ::: "memory");  // all reads of S_cc precede the write
-        scan[cc * D + c] = acc;
-      }
-      asm volatile("" ::: "memory");
-    }
-  }
-  block_sync<W>();
-  if (c > 0) {
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-      s1[k] = scan[(c - 1) * D + 2 * k];
-      s2[k] = scan[(c - 1) * D + 2 * k + 1];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
-  }
-  block_sync<W>();  // W > 1: states read before the tiles are reused
+  carry_scan<S, W>(scan, e, s1, s2, sp, c, C);
 
   // ---- pass 2: outputs from the carried state
   run_pass<S, kApply, kWave, VM, (VM > 0), NORM, AFF>(x, y, rsrc, tile, rows, io2, T, lane, s1,
                                                       s2, e, p, G, clip);
+}
+
+// ---------------------------------------------------------------------------
+// Fused SRC + cascade (chain fast path, dsp_chain_f32): ONE launch computes
+// y = SRC(x) and z = clip(EQ(y)) for a channel per wavefront without ever
+// reading y back from HBM.  Pass 1 and the carry scan are those of
+// k_iir_wave<P1 = 2> (chunk states straight from x); pass 2 then recomputes
+// the chunk's SRC outputs from x in registers, stores them (the drop-in API
+// returns y), runs the cascade on them and stores z.  HBM traffic per channel:
+// x twice (pass 1's overlapping rows, pass 2) + y + z, against x + y (SRC
+// kernel) + x + y + z (cascade) for the two-launch chain.
+//
+// SRC geometry for a compile-time (L, M, TT = ceil(K/L), BQ = c mod L):
+// lane c owns outputs m = c*T + t.  A pass-2 tile is NOUT = 32*L/M outputs,
+// i.e. exactly 32 new input samples, so every tile has the same phase pattern:
+// output i of tile k reads x[c*T*M/L + 32k + a + q(i) - u] (a = c div L,
+// q(i) = (i*M + BQ) div L) with the taps P[phi(i)][u], phi(i) = (i*M+BQ) mod L.
+// The lane keeps the window of WL = q(NOUT-1) + TT samples in registers: the
+// last CR = WL - 32 carry over, 32 new ones come from the coalesced x tile in
+// LDS.  Accumulation order is exactly k_src_reg's (taps reversed, one fmaf
+// chain per output from 0), so y is bitwise the SRC kernel's.
+// ---------------------------------------------------------------------------
+template <int L_, int M_, int TT_, int BQ_>
+struct SrcGeo {
+  static constexpr int L = L_, M = M_, TT = TT_, BQ = BQ_;
+  static_assert((kTS * L) % M == 0, "32 input samples must make whole outputs");
+  static_assert(L <= 4, "one float4 of taps per tap index");
+  static constexpr int NOUT = kTS * L / M;  // outputs per tile
+  static_assert(NOUT % 4 == 0, "float4 stores");
+  static constexpr int q(int i) { return (i * M + BQ) / L; }
+  static constexpr int phi(int i) { return (i * M + BQ) % L; }
+  static constexpr int WL = q(NOUT - 1) + TT;  // window (input samples)
+  static constexpr int CR = WL - kTS;          // carried between tiles
+  static_assert(CR >= 0, "window shorter than a tile");
+  static constexpr int PRO = (CR + kTS - 1) / kTS;  // prologue tiles
+  static constexpr int OROW = NOUT + 1;        // LDS row stride of the y/z tile (odd)
+};
+
+// Pass-2 inputs of the fused kernel.
+struct FusedSrc {
+  float* y;            // SRC output rows (pitch = z's)
+  const float* taps;   // float32 L*h[K] (dsp_core.py:162)
+  int K;
+  int64_t nb0;         // channel-relative x index of chunk 0's first prologue block
+};
+
+// Stores the wave's 64-row x NOUT-float tile (LDS row stride OROW) to the
+// rows' [t0, t0 + NOUT) ranges: consecutive lanes take consecutive float4s of
+// a row, so each instruction writes ~NOUT*4-byte contiguous runs.  The buffer
+// resource spans one channel's row; stores past its end are dropped.
+#if DSP_CHAIN_EXP == 4 || DSP_CHAIN_EXP == 5
+constexpr int kNstExp = 32;  // ablation: 32 of the NOUT outputs stored
+#else
+constexpr int kNstExp = 0;
+#endif
+template <class SG>
+__device__ __forceinline__ void store_rows(__amdgpu_buffer_rsrc_t rs, const float* tile,
+                                           int64_t T, int t0, int lane) {
+  constexpr int V = (kNstExp ? kNstExp : SG::NOUT) / 4;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int s = 0; s < V; ++s) {
+    const int e = s * kWave + lane;
+    const int row = e / V, c4 = (e - row * V) * 4;
+    const float* src = tile + row * SG::OROW + c4;
+    u32x4 d;
+    d.x = __float_as_uint(src[0]);
+    d.y = __float_as_uint(src[1]);
+    d.z = __float_as_uint(src[2]);
+    d.w = __float_as_uint(src[3]);
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(((int64_t)row * T + t0 + c4) * 4), 0, 0);
+  }
+}
+
+template <int S, class SG>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2))) void k_chain_wave(
+    float* __restrict__ z, int64_t n, int64_t ld, SosParams p, ScanParams sp,
+    const double* __restrict__ G, int64_t T, int C, int clip, XState XS, FusedSrc FS) {
+  constexpr int D = 2 * S;
+  constexpr int NOUT = SG::NOUT, WL = SG::WL, CR = SG::CR, PRO = SG::PRO;
+  constexpr int TILE = (kWave * SG::OROW > kWaveTileFloats ? kWave * SG::OROW : kWaveTileFloats);
+  static_assert(kWave * D * 2 <= TILE, "scan must fit in the tile");
+  __shared__ __attribute__((aligned(16))) float tile[TILE];
+  __shared__ __attribute__((aligned(16))) float s_bank[SG::TT * 4];
+  __shared__ int64_t s_in[kWave], s_out[kWave];
+  __shared__ int s_len[kWave], s_lo[kWave];
+  double* scan = reinterpret_cast<double*>(tile);
+
+  const int c = threadIdx.x;  // chunk
+  const int64_t b = blockIdx.x;
+  // Tap bank: s_bank[v][p] = P[p][TT-1-v] = taps[p + L*(TT-1-v)] (0 past K).
+  for (int i = c; i < SG::TT * 4; i += kWave) {
+    const int v = i >> 2, ph = i & 3, k = ph + SG::L * (SG::TT - 1 - v);
+    s_bank[i] = (ph < SG::L && k < FS.K) ? FS.taps[k] : 0.f;
+  }
+  // Pass-1 rows: the x-domain state windows (k_iir_wave<P1 = 2>).
+  {
+    const int64_t start = (int64_t)c * XS.shift + XS.q0;
+    const bool need = c + 1 < C;
+    s_in[c] = need ? b * XS.ld + start : 0;
+    s_lo[c] = need ? (int)max((int64_t)0, -start) : 0;
+    s_len[c] = need ? (int)max((int64_t)0, min(XS.rows, XS.n - start)) : 0;
+    s_out[c] = 0;
+  }
+  const Rows rows{s_in, s_out, s_len, s_lo};
+  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(XS.xs) + b * XS.ld, 0, (int)(XS.n * 4), 0x00020000);
+  const AffIO io1 = aff_rows(xin, XS.shift, XS.q0, 0, 0, c);
+
+  double s1[S], s2[S], e[D];
+#pragma unroll
+  for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) e[i] = 0.0;
+  const __amdgpu_buffer_rsrc_t zr =
+      __builtin_amdgcn_make_buffer_rsrc(z + b * ld, 0, (int)(n * 4), 0x00020000);
+
+  // ---- pass 1: zero-state end state of the lane's chunk, from x
+#if DSP_CHAIN_EXP != 6
+  run_pass<S, kStateTable, kWave, 1, true, true, true>(XS.xs, z, zr, tile, rows, io1, XS.rows, c,
+                                                       s1, s2, e, p, G, clip);
+#endif
+  // ---- carry scan
+  carry_scan<S, 1>(scan, e, s1, s2, sp, c, C);
+
+  // ---- pass 2: y = SRC(x) for the chunk, z = clip(cascade(y))
+  const AffIO io2 = aff_rows(xin, XS.shift, FS.nb0, 0, 0, c);
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc(FS.y + b * ld, 0, (int)(n * 4), 0x00020000);
+  const float clo = clip ? -1.f : -INFINITY, chi = clip ? 1.f : INFINITY;
+  const int steps = PRO + (int)(T / NOUT);
+  const float* my = tile + c * kRow;
+  float* orow = tile + c * SG::OROW;
+  float win[WL];
+#pragma unroll
+  for (int i = 0; i < WL; ++i) win[i] = 0.f;
+  // Every path into the loop header has the next tile's loads followed by
+  // exactly 2*NOUT/4 stores (prologue tiles store out of range, the last
+  // tile's fetch reads out of range), so the compiler's wait for the loads is
+  // vmcnt(2*NOUT/4) and never drains the previous tile's y/z stores.
+  constexpr int kFar = 1 << 28;  // sample offset beyond any row: OOB, no traffic
+  float4 v[kLoads];
+  fetch_aff(v, io2, 0);
+  store_rows<SG>(yr, tile, T, kFar, c);
+  store_rows<SG>(zr, tile, T, kFar, c);
+  for (int kk = 0; kk < steps; ++kk) {
+    asm volatile("" ::: "memory");  // the previous tile's LDS reads come first
+    tile_put<kWave, false>(tile, v, rows, 0, c);
+    asm volatile("" ::: "memory");
+    fetch_aff(v, io2, kk + 1 < steps ? (kk + 1) * kTS : kFar);
+#pragma unroll
+    for (int i = 0; i < CR; ++i) win[i] = win[i + kTS];
+#pragma unroll
+    for (int j = 0; j < kTS; ++j) win[CR + j] = my[j];
+    if (kk < PRO) {
+      store_rows<SG>(yr, tile, T, kFar, c);
+      store_rows<SG>(zr, tile, T, kFar, c);
+      continue;
+    }
+#if DSP_CHAIN_EXP == 4
+    const int t0 = (kk - PRO) * 32;  // ablation: line-aligned partial stores
+#else
+    const int t0 = (kk - PRO) * NOUT;
+#endif
+    float acc[NOUT];
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) acc[i] = 0.f;
+#if DSP_CHAIN_EXP == 1
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) acc[i] = win[SG::q(i)] * 0.5f;
+#pragma unroll
+    for (int u = 0; u < 0; ++u) {
+#else
+#pragma unroll
+    for (int u = 0; u < SG::TT; ++u) {
+#endif
+      const float4 tq = *reinterpret_cast<const float4*>(s_bank + 4 * u);
+      const float tp[4] = {tq.x, tq.y, tq.z, tq.w};
+#pragma unroll
+      for (int i = 0; i < NOUT; ++i) acc[i] = fmaf(tp[SG::phi(i)], win[SG::q(i) + u], acc[i]);
+    }
+    asm volatile("" ::: "memory");  // x tile reads done before the y tile overwrites it
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) orow[i] = acc[i];
+    asm volatile("" ::: "memory");
+#if DSP_CHAIN_EXP != 3
+    store_rows<SG>(yr, tile, T, t0, c);
+#endif
+    asm volatile("" ::: "memory");  // y reads done before z overwrites the tile
+#if DSP_CHAIN_EXP == 2
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) orow[i] = clip_f32(acc[i] * 0.25f, clo, chi);
+#else
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i)
+      orow[i] = clip_f32((float)cascade_step<S, true>((double)acc[i], s1, s2, p), clo, chi);
+#endif
+    asm volatile("" ::: "memory");
+#if DSP_CHAIN_EXP != 3
+    store_rows<SG>(zr, tile, T, t0, c);
+#else
+    if (clip == 12345) store_rows<SG>(zr, tile, T, t0, c);
+#endif
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -940,6 +1158,64 @@ int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t
                                     XS, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
+}
+
+namespace {
+bool x_aligned(const void* ptr, int64_t ld) {
+  return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(ptr) & 15) == 0;
+}
+
+template <int S, class SG>
+int run_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n, int64_t ld,
+                    const SosParams& p, int clip, int64_t T, const double* gx, const XState& XS,
+                    const float* taps, int K, int64_t a, hipStream_t s) {
+  ScanParams sp;
+  const std::vector<double> P = chunk_transition(p, S, T);
+  for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
+  const int C = (int)ceil_div(n, T);
+  // Chunk 0's first new-sample block: window start a - (TT-1), plus the carry,
+  // minus the prologue blocks.
+  FusedSrc FS{y, taps, K, a - (SG::TT - 1) + SG::CR - (int64_t)kTS * SG::PRO};
+  TraceScope trace("chain_fused", s);
+  hipLaunchKernelGGL((k_chain_wave<S, SG>), dim3((unsigned)B), dim3(kWave), 0, s, z, n, ld, p,
+                     sp, gx, T, C, clip, XS, FS);
+  DSP_LAUNCHED("k_chain_wave");
+  return DSP_OK;
+}
+}  // namespace
+
+int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
+                       int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
+                       int L, int M, int64_t c, const double* sos, int S, int clip,
+                       int64_t chunk_len, const double* gx, int64_t gx_rows, hipStream_t s) {
+  // Instantiated geometries: (L, M, ceil(K/L), c mod L) of the benchmark
+  // configurations 3/4 (3/2, K = 121) and the app's 2/1 with the default
+  // K = 81.  Anything else takes the two-launch chain.
+  const int TT = (K + L - 1) / L;
+  const int64_t a = c / L, bq = c % L;
+  int geo = 0;
+  if (L == 3 && M == 2 && TT == 41 && bq == 0) geo = 1;
+  if (L == 2 && M == 1 && TT == 41 && bq == 0) geo = 2;
+  if (!geo || S != 6 || !gx || !sos || !x_aligned(xs, ld_xs) || !x_aligned(y, ld_y) ||
+      !x_aligned(z, ld_y) || n_in % 4 || n_out % 4 || n_in * 4 + 16 >= (int64_t)kOob ||
+      n_out * 4 + 16 >= (int64_t)kOob || ld_xs < n_in || ld_y < n_out)
+    return kNotFused;
+  const int nout = geo == 1 ? SrcGeo<3, 2, 41, 0>::NOUT : SrcGeo<2, 1, 41, 0>::NOUT;
+  const int cr = geo == 1 ? SrcGeo<3, 2, 41, 0>::CR : SrcGeo<2, 1, 41, 0>::CR;
+  if (chunk_len % nout || (a - (TT - 1) + cr) % 4 != 0) return kNotFused;
+  const int64_t C = ceil_div(n_out, chunk_len);
+  if (!fused_ok(S, C, chunk_len) || C > kWave) return kNotFused;
+  SosParams p;
+  if (!realize(sos, S, &p)) return kNotFused;
+  XState XS{xs, ld_xs, n_in, 0, 0, 0};
+  if (int rc = xstate_geometry(chunk_len, K, L, M, c, &XS.shift, &XS.q0, &XS.rows)) return rc;
+  DSP_REQUIRE(gx_rows == XS.rows, "x-domain state table has %lld rows, geometry needs %lld",
+              (long long)gx_rows, (long long)XS.rows);
+  if (geo == 1)
+    return run_chain_fused<6, SrcGeo<3, 2, 41, 0>>(xs, y, z, B, n_out, ld_y, p, clip, chunk_len,
+                                                   gx, XS, taps, K, a, s);
+  return run_chain_fused<6, SrcGeo<2, 1, 41, 0>>(xs, y, z, B, n_out, ld_y, p, clip, chunk_len,
+                                                 gx, XS, taps, K, a, s);
 }
 
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len) {

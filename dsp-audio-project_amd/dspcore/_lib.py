@@ -60,6 +60,7 @@ _SIGNATURES = {
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,
         _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "dsp_chain_fusion": (ctypes.c_int, [_c_i32]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i64]),
     "dsp_chain_xstate_geometry": (ctypes.c_int, [
         _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64),
@@ -129,6 +130,12 @@ def check(rc: int, what: str) -> None:
     if rc == DSP_EINVAL:
         raise ValueError(msg)
     raise RuntimeError(msg)
+
+
+def chain_fusion(mode: int = -1) -> bool:
+    """Fused SRC + cascade launch of dsp_chain_f32 on the calling thread
+    (dsp_chain_fusion): 0 off, 1 on, -1 query.  Returns the previous setting."""
+    return bool(load().dsp_chain_fusion(int(mode)))
 
 
 def trace_enable(on: bool) -> None:

@@ -161,7 +161,18 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * chunk_len*M/L an integer multiple of 4 and 16-byte aligned rows of x.
  * Otherwise `state_table` (G, may be NULL) is used as in
  * dsp_biquad_cascade_f32.
+ *
+ * Fusion (opt-in).  With the x-domain states, S == 6, n_in and n_out
+ * multiples of 4, 16-byte aligned rows and an instantiated SRC geometry
+ * ((L, M, ceil(K/L), c_offset mod L) = (3, 2, 41, 0) or (2, 1, 41, 0)), SRC
+ * and cascade can run as ONE launch that computes y from x in registers,
+ * stores it and filters it (y is never read back); y is bitwise the separate
+ * SRC kernel's, z that of the two-launch chain.  It moves 23 % fewer HBM bytes
+ * but measures slower on MI355X, so it is off by default:
+ * dsp_chain_fusion(1) turns it on for the calling thread, dsp_chain_fusion(0)
+ * off; it returns the previous setting, dsp_chain_fusion(-1) only queries it.
  * ------------------------------------------------------------------------- */
+int dsp_chain_fusion(int32_t mode);
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S,
                                  int64_t chunk_len);
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,

@@ -376,3 +376,48 @@ def test_shard_driver_bitwise_invariant(gpu):
         got = run_sharded(fn, x, [gpu] * parts)
         for a, b in zip(got, base):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("L,M", [(3, 2), (2, 1)])
+def test_chain_fused_launch_matches_two_launch(gpu, L, M):
+    """The fused SRC + cascade launch (dsp_chain_fusion on) against the
+    two-launch chain (off) on the same plan: y, z and |X| bitwise equal, the
+    fused kernel is the one that ran, and rows match the reference recipe."""
+    from dspcore import _lib
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.design import xstate_chunk_len
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 6, 48000
+    cfg = ChainConfig(n_in, 48000, L, M, None, orc.CONFIG3_GAINS, n_fft=4096)
+    n_out = n_in * L // M
+    ch = Chain(cfg, B, gpu, chunk_len=xstate_chunk_len(n_out, L, M, 64))
+    assert ch.xstate and -(-n_out // ch.chunk_len) <= 64
+    gen = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[1] *= 40.0                      # drive the clip
+    x[2, : n_in // 2] = 0.0           # silence then signal
+    runs = {}
+    prev = _lib.chain_fusion(-1)
+    try:
+        for mode in (1, 0):
+            _lib.chain_fusion(mode)
+            _lib.trace_enable(True)
+            _lib.trace_read()
+            y, z, mag = (t.clone() for t in ch.run(x))
+            names = [n for n, _ in _lib.trace_read()]
+            _lib.trace_enable(False)
+            runs[mode] = (y, z, mag, names)
+    finally:
+        _lib.chain_fusion(int(prev))
+    assert "chain_fused" in runs[1][3] and "src_poly" not in runs[1][3]
+    assert "chain_fused" not in runs[0][3]
+    for a, b in zip(runs[1][:3], runs[0][:3]):
+        assert torch.equal(a, b)
+    y, z, mag = (t.cpu().numpy() for t in runs[1][:3])
+    assert np.abs(z[1]).max() == 1.0
+    for b in (0, 1, 2):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, L, M, orc.CONFIG3_GAINS,
+                                       None, 4096)
+        assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)

@@ -16,6 +16,8 @@ def short(name):
     """Bench-trace name of a libdspcore kernel from its demangled symbol."""
     if "k_src" in name:
         return "src_poly"
+    if "k_chain_wave" in name:
+        return "chain_fused"
     m = re.search(r"k_iir_wave<(\d+), (\d+)", name)
     if m:
         return "iir_xstate" if m.group(2) == "2" else "iir_fused"
