@@ -1,10 +1,17 @@
-# Builds libdspcore variants with extra -D flags: bash tools/build_variants.sh NAME "FLAGS" ...
+# Builds libdspcore variants with extra -D flags on one source (SRC=iir by default):
+#   [SRC=src_poly] bash tools/build_variants.sh NAME "FLAGS" ...
 set -e
 cd "$(dirname "$0")/../dsp-audio-project_amd/csrc"
+src=${SRC:-iir}
 mkdir -p ../build/var
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -I. -fno-slp-vectorize $flags -c iir.hip -o ../build/var/iir_$name.o &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/libdspcore_$name.so ../build/abi.o ../build/src_poly.o ../build/var/iir_$name.o ../build/fft.o ../build/audio_io.o && echo built $name ) &
+  objs=""
+  for f in abi src_poly iir fft audio_io; do
+    if [ "$f" = "$src" ]; then objs="$objs ../build/var/${f}_$name.o"; else objs="$objs ../build/$f.o"; fi
+  done
+  extra=""; [ "$src" = iir ] && extra="-fno-slp-vectorize"
+  ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -I. $extra $flags -c $src.hip -o ../build/var/${src}_$name.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/libdspcore_$name.so $objs && echo built $name ) &
 done
 wait
