@@ -134,6 +134,8 @@ def kernel_bytes(chain, name):
     N = chain.spec.n_fft
     return {
         "src_poly": 4 * B * (n_in + n_out),
+        "src_states": 4 * B * (n_in + n_out),           # + 2 float64 states per chunk
+        "iir_ystate": 8 * B * n_out,
         "iir_state": 4 * B * (C - 1) * T + 8 * 2 * S * B * (C - 1),
         "iir_carry": 8 * 2 * S * B * (2 * C - 1),
         "iir_apply": 8 * B * n_out + 8 * 2 * S * B * C,

@@ -22,7 +22,10 @@ struct TraceState {
   size_t used = 0;
 };
 thread_local TraceState g_trace;
-thread_local bool g_chain_fusion = false;  // measured slower
+// dsp_chain_fusion: 0 x-domain chunk states (default), 1 fused SRC + cascade
+// launch, 2 chunk states emitted by the SRC kernel (1 and 2 measured slower,
+// DESIGN.md §3.5).
+thread_local int g_chain_mode = 0;
 }  // namespace
 
 TraceScope::TraceScope(const char* name, hipStream_t s) : slot_(-1), s_(s) {
@@ -131,13 +134,16 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_
 
 int dsp_chain_fusion(int32_t mode) {
   dsp::clear_error();
-  const int prev = dsp::g_chain_fusion ? 1 : 0;
-  if (mode >= 0) dsp::g_chain_fusion = mode != 0;
+  if (mode < -1 || mode > 2) return dsp::set_error(DSP_EINVAL, "chain mode %d not in [-1, 2]", mode);
+  const int prev = dsp::g_chain_mode;
+  if (mode >= 0) dsp::g_chain_mode = mode;
   return prev;
 }
 
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
-  return dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+  const size_t a = dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+  const size_t b = (2 * S == dsp::kStD) ? dsp::chain_states_bytes(B, n_out, chunk_len) : 0;
+  return a > b ? a : b;
 }
 
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
@@ -160,9 +166,13 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
   if (B == 0) return DSP_OK;
   int rc = dsp::kNotFused;
-  if (xstate_table && S > 0 && dsp::g_chain_fusion)
+  if (xstate_table && S > 0 && dsp::g_chain_mode == 1)
     rc = dsp::launch_chain_fused(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
                                  sos_host, S, clip, chunk_len, xstate_table, xstate_rows, s);
+  else if (S > 0 && dsp::g_chain_mode == 2)
+    rc = dsp::launch_chain_ystate(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
+                                  sos_host, S, clip, chunk_len, state_table, workspace,
+                                  workspace_bytes, s);
   if (rc == DSP_OK)
     return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
                                 twiddles, s);

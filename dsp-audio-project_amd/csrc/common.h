@@ -39,6 +39,7 @@ void clear_error();
   } while (0)
 
 constexpr int kWave = 64;
+constexpr int kNotFused = 1;  // a fast path's launcher declined; nothing was launched
 
 // RAII bracket of one kernel launch for dsp_trace_* (no-op unless enabled on
 // this thread).
@@ -94,7 +95,39 @@ int launch_dft(const float* in, float* out, int64_t B, int64_t n, int real_in, i
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
-// Fused cascade whose chunk end states E[B][C-1][2S] were produced upstream.
+
+// Chain mode 2 (dsp_chain_fusion): the SRC kernel emits the cascade's chunk end
+// states from the y tile it already holds in LDS, so the cascade skips its
+// first pass.  A tile of TILE outputs is cut into sub-chunks of kStU samples;
+// sub-chunk j's zero-state end state is s_j = sum_t g[t] y[kStU*j + t] with
+// g[t] = A^(kStU-1-t) b (the last kStU rows of the y-domain state table G of
+// chunk_len), and every chunk piece the tile holds is carried to the chunk's
+// end by Horner steps S <- A^kStU S + s_j.  A chunk overlaps at most two tiles
+// (chunk_len <= TILE): part[b][c][slot][kStD], slot = tile - first tile of c,
+// and the cascade sums the two slots in that order (deterministic).
+constexpr int kStU = 96;       // sub-chunk length
+constexpr int kStD = 12;       // state dimension (S = 6 stages)
+constexpr int kStPieces = 12;  // chunk pieces per tile (16 lanes each, 192 threads)
+struct SrcStates {
+  double* part;             // [B][C][2][kStD]
+  const double* g;          // [kStU][kStD], device
+  double AU[kStD * kStD];   // A^kStU, row-major
+  int64_t chunk_len;
+  int C;
+};
+// SRC with state emission; kNotFused (nothing launched) unless the geometry
+// is instantiated ((L, M, ceil(K/L)) = (3, 2, 41)).
+int launch_src_states(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
+                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
+                      int64_t c, const SrcStates& st, hipStream_t s);
+int src_states_tile(int L, int M, int K);  // TILE of that instantiation, 0 if none
+size_t chain_states_bytes(int64_t B, int64_t n_out, int64_t chunk_len);
+// SRC (emitting states) + cascade reading them; kNotFused if not applicable.
+int launch_chain_ystate(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
+                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
+                        int L, int M, int64_t c, const double* sos, int S, int clip,
+                        int64_t chunk_len, const double* state_table, void* ws,
+                        size_t ws_bytes, hipStream_t s);
 // Audio I/O (audio_io.hip).
 int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames);
@@ -111,7 +144,6 @@ int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* 
                     int64_t* q0, int64_t* rows);
 // Fused SRC + cascade (one launch, y never re-read).  Returns kNotFused, with
 // nothing launched, when the geometry has no instantiation.
-constexpr int kNotFused = 1;
 int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
                        int L, int M, int64_t c, const double* sos, int S, int clip,

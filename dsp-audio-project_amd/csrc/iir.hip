@@ -425,9 +425,14 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 // (dspcore/design.py:xstate_table).  Pass 1 then reads the SRC input (2/3 of
 // the bytes at L/M = 3/2) and costs 2S*M/L FMAs per output sample instead of
 // 2S, and the chunk states are those of the exact float64 SRC output.
+// P1 = 3 (chain mode 2): the end states come from the SRC kernel, two pieces
+// per chunk (common.h SrcStates): part[b][c][slot][2S], slot 1 present when the
+// chunk reaches into the SRC tile after the one holding its start.
 struct XState {
   const float* xs;  // SRC input rows [B][ld]
   int64_t ld, n, shift, q0, rows;
+  const double* part;  // P1 = 3
+  int64_t tile;        // P1 = 3: SRC tile length
 };
 
 // Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
@@ -552,7 +557,22 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   constexpr bool AFF = VM > 0;
-  if constexpr (P1 == 2) {
+  static_assert(P1 != 3 || D == kStD, "SRC-emitted states are 12-dimensional");
+  if constexpr (P1 == 3) {
+    // Emitted by the SRC kernel: slot 0 from the tile holding the chunk's
+    // start, slot 1 from the next tile if the chunk reaches into it; summed in
+    // that order.
+    if (c + 1 < C) {
+      const double* e0 = XS.part + (b * C + c) * 2 * D;
+      const bool two = t_begin / XS.tile != (t_begin + T - 1) / XS.tile;
+#pragma unroll
+      for (int i = 0; i < D; ++i) e[i] = e0[i];
+      if (two) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) e[i] += e0[D + i];
+      }
+    }
+  } else if constexpr (P1 == 2) {
     run_pass<S, kStateTable, kWave, VM, true, NORM, AFF>(XS.xs, y, rsrc, tile, rows, io1,
                                                          XS.rows, lane, s1, s2, e, p, G, clip);
   } else if constexpr (P1 == 1) {
@@ -597,8 +617,9 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
 // q(i) = (i*M + BQ) div L) with the taps P[phi(i)][u], phi(i) = (i*M+BQ) mod L.
 // The lane keeps the window of WL = q(NOUT-1) + TT samples in registers: the
 // last CR = WL - 32 carry over, 32 new ones come from the coalesced x tile in
-// LDS.  Accumulation order is exactly k_src_reg's (taps reversed, one fmaf
-// chain per output from 0), so y is bitwise the SRC kernel's.
+// LDS.  Accumulation is one fmaf chain per output over the reversed taps, i.e.
+// k_src_reg's scalar order (DSP_SRC_PACK=0); the default SRC kernel pairs taps
+// in v_pk_fma_f32, so y agrees with it to float32 rounding.
 // ---------------------------------------------------------------------------
 template <int L_, int M_, int TT_, int BQ_>
 struct SrcGeo {
@@ -1006,7 +1027,7 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const std::vector<double> P = chunk_transition(p, S, T);
   for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
   const int C = (int)ceil_div(n, T);
-  TraceScope trace(p1mode == 2 ? "iir_xstate" : "iir_fused", s);
+  TraceScope trace(p1mode == 2 ? "iir_xstate" : p1mode == 3 ? "iir_ystate" : "iir_fused", s);
   // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
   // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
   // address one channel's row with a 31-bit byte offset.
@@ -1030,6 +1051,10 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   // The state tables are built for the NORM realisation (the EQ's); a cascade
   // with some b0 == 0 runs pass 1 as the cascade itself.
   if (!norm) { DSP_WAVE_VM(0, false) }
+  else if (p1mode == 3) {
+    if constexpr (2 * S == kStD) { DSP_WAVE_VM(3, true) }
+    else return set_error(DSP_EINVAL, "SRC-emitted chunk states need S = %d", kStD / 2);
+  }
   else if (p1mode == 2) { DSP_WAVE_VM(2, true) }
   else if (p1mode == 1) { DSP_WAVE_VM(1, true) }
   else { DSP_WAVE_VM(0, true) }
@@ -1216,6 +1241,42 @@ int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n
                                                    gx, XS, taps, K, a, s);
   return run_chain_fused<6, SrcGeo<2, 1, 41, 0>>(xs, y, z, B, n_out, ld_y, p, clip, chunk_len,
                                                  gx, XS, taps, K, a, s);
+}
+
+size_t chain_states_bytes(int64_t B, int64_t n_out, int64_t chunk_len) {
+  if (B <= 0 || n_out <= 0 || chunk_len <= 0) return 0;
+  return (size_t)B * (size_t)ceil_div(n_out, chunk_len) * 2 * kStD * sizeof(double);
+}
+
+int launch_chain_ystate(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
+                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
+                        int L, int M, int64_t c, const double* sos, int S, int clip,
+                        int64_t chunk_len, const double* state_table, void* ws,
+                        size_t ws_bytes, hipStream_t s) {
+  const int64_t tile = src_states_tile(L, M, K);
+  const int64_t C = chunk_len > 0 ? ceil_div(n_out, chunk_len) : 0;
+  if (!tile || 2 * S != kStD || !sos || !state_table || chunk_len <= 0 ||
+      chunk_len % kStU || chunk_len > tile || ceil_div(tile - 1, chunk_len) + 1 > kStPieces ||
+      !fused_ok(S, C, chunk_len) || ld_y < n_out || !ws ||
+      ws_bytes < chain_states_bytes(B, n_out, chunk_len) ||
+      (reinterpret_cast<uintptr_t>(ws) & 7))
+    return kNotFused;
+  SosParams p;
+  if (!realize(sos, S, &p)) return kNotFused;
+  SrcStates st;
+  st.part = static_cast<double*>(ws);
+  st.g = state_table + (chunk_len - kStU) * kStD;  // G[T - kStU + t] = A^(kStU-1-t) b
+  const std::vector<double> AU = chunk_transition(p, S, kStU);
+  for (int i = 0; i < kStD * kStD; ++i) st.AU[i] = AU[i];
+  st.chunk_len = chunk_len;
+  st.C = (int)C;
+  if (int rc = launch_src_states(xs, y, B, n_in, ld_xs, n_out, ld_y, taps, K, L, M, c, st, s))
+    return rc;
+  XState XS{};
+  XS.part = st.part;
+  XS.tile = tile;
+  return run_fused<6>(y, z, B, n_out, ld_y, ld_y, p, true, clip, chunk_len, state_table, 3,
+                      x_aligned(y, ld_y), x_aligned(z, ld_y), XS, s);
 }
 
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len) {

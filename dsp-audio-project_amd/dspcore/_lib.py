@@ -132,10 +132,15 @@ def check(rc: int, what: str) -> None:
     raise RuntimeError(msg)
 
 
-def chain_fusion(mode: int = -1) -> bool:
-    """Fused SRC + cascade launch of dsp_chain_f32 on the calling thread
-    (dsp_chain_fusion): 0 off, 1 on, -1 query.  Returns the previous setting."""
-    return bool(load().dsp_chain_fusion(int(mode)))
+def chain_fusion(mode: int = -1) -> int:
+    """Chain mode of dsp_chain_f32 on the calling thread (dsp_chain_fusion):
+    0 x-domain chunk states, 1 fused SRC + cascade launch, 2 chunk states
+    emitted by the SRC kernel (default); -1 only queries.  Returns the
+    previous mode."""
+    rc = load().dsp_chain_fusion(int(mode))
+    if rc < 0:
+        check(rc, "dsp_chain_fusion")
+    return rc
 
 
 def trace_enable(on: bool) -> None:

@@ -162,15 +162,23 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * Otherwise `state_table` (G, may be NULL) is used as in
  * dsp_biquad_cascade_f32.
  *
- * Fusion (opt-in).  With the x-domain states, S == 6, n_in and n_out
- * multiples of 4, 16-byte aligned rows and an instantiated SRC geometry
- * ((L, M, ceil(K/L), c_offset mod L) = (3, 2, 41, 0) or (2, 1, 41, 0)), SRC
- * and cascade can run as ONE launch that computes y from x in registers,
- * stores it and filters it (y is never read back); y is bitwise the separate
- * SRC kernel's, z that of the two-launch chain.  It moves 23 % fewer HBM bytes
- * but measures slower on MI355X, so it is off by default:
- * dsp_chain_fusion(1) turns it on for the calling thread, dsp_chain_fusion(0)
- * off; it returns the previous setting, dsp_chain_fusion(-1) only queries it.
+ * Chain modes, per calling thread (dsp_chain_fusion sets 0, 1 or 2 and returns
+ * the previous mode, -1 only queries, anything else is DSP_EINVAL):
+ *   0 (default)  SRC, then the cascade with the chunk states above;
+ *   1  with the x-domain states, S == 6, n_in and n_out multiples of 4,
+ *      16-byte aligned rows and an instantiated SRC geometry ((L, M, ceil(K/L),
+ *      c_offset mod L) = (3, 2, 41, 0) or (2, 1, 41, 0)): ONE launch computes y
+ *      from x in registers, stores it and filters it (y is never read back);
+ *      y is bitwise the default SRC kernel's, z that of mode 0.  23 % fewer HBM
+ *      bytes, measured slower;
+ *   2  with `state_table` (G of chunk_len), S == 6, (L, M, ceil(K/L)) =
+ *      (3, 2, 41), chunk_len a multiple of 96 in [288, 2880] and
+ *      ceil(n_out / chunk_len) <= 256: the SRC kernel also emits every chunk's
+ *      end state from the y tiles it holds (two float64 pieces per chunk in
+ *      `workspace`) and the cascade skips its first pass; y is bitwise mode 0's,
+ *      z equal to float64 rounding.  The cascade gets 30 % faster, the SRC
+ *      twice as slow: measured slower.
+ * A mode whose conditions do not hold runs as mode 0.
  * ------------------------------------------------------------------------- */
 int dsp_chain_fusion(int32_t mode);
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S,

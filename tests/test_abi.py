@@ -130,3 +130,17 @@ def test_wav_header_matches_scipy_writer():
     hdr = ctypes.create_string_buffer(44)
     assert _lib.load().dsp_wav_header_pcm16(hdr, 72000, 1, pcm.size) == 0
     assert hdr.raw + pcm.tobytes() == buf.getvalue()
+
+
+def test_chain_mode_and_workspace_query():
+    """dsp_chain_fusion takes modes 0-2 (-1 queries); the chain workspace holds
+    the SRC-emitted chunk states (two float64 12-vectors per chunk)."""
+    lib = _lib.load()
+    prev = lib.dsp_chain_fusion(-1)
+    assert prev in (0, 1, 2)
+    assert lib.dsp_chain_fusion(3) == _lib.DSP_EINVAL
+    assert lib.dsp_chain_fusion(-1) == prev
+    B, n, T = 4096, 72000, 1152
+    C = -(-n // T)
+    assert lib.dsp_chain_workspace_bytes(B, n, 6, T) >= B * C * 2 * 12 * 8
+    assert lib.dsp_chain_workspace_bytes(B, n, 0, T) == 0

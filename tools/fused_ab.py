@@ -37,5 +37,5 @@ for rnd in range(3):
         for k, ms in recs:
             res.setdefault((mode, k), []).append(ms)
 print(os.path.basename(_lib.LIB_PATH), f"L/M={L}/{M}",
-      {f"{'F' if m else 'U'}:{k}": round(float(np.median(v)), 4) for (m, k), v in res.items()},
+      {f"m{m}:{k}": round(float(np.median(v)), 4) for (m, k), v in res.items()},
       "z00", float(ch.z[0, 1000]))
