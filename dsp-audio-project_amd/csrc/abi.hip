@@ -179,7 +179,9 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   if (rc != dsp::kNotFused) return rc;
   rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
   if (rc) return rc;
-  if (xstate_table && S > 0)
+  // The x-domain states need aligned input rows and a fitting chunking;
+  // otherwise the y-domain table serves (include/dspcore.h).
+  if (xstate_table && dsp::xstate_applicable(n_out, S, chunk_len, x, ld_x, L, M))
     rc = dsp::launch_biquad_xstate(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len, x,
                                    n_in, ld_x, K, L, M, c_offset, xstate_table, xstate_rows, s);
   else

@@ -148,6 +148,10 @@ int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n
                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
                        int L, int M, int64_t c, const double* sos, int S, int clip,
                        int64_t chunk_len, const double* gx, int64_t gx_rows, hipStream_t s);
+// Whether launch_biquad_xstate's conditions on the cascade (n, S, chunk_len)
+// and on the SRC input rows (16-byte aligned) hold.
+bool xstate_applicable(int64_t n, int S, int64_t chunk_len, const float* xs, int64_t ld_xs,
+                       int L, int M);
 int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
                          int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
                          const float* xs, int64_t n_in, int64_t ld_xs, int K, int L, int M,

@@ -1146,6 +1146,14 @@ int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* 
   return DSP_OK;
 }
 
+bool xstate_applicable(int64_t n, int S, int64_t chunk_len, const float* xs, int64_t ld_xs,
+                       int L, int M) {
+  if (S < 1 || S > 8 || S == 7 || chunk_len <= 0 || chunk_len % kTS) return false;
+  if ((chunk_len * M) % L || ((chunk_len * M) / L) % 4) return false;
+  if ((ld_xs & 3) || (reinterpret_cast<uintptr_t>(xs) & 15)) return false;
+  return fused_ok(S, ceil_div(n, chunk_len), chunk_len);
+}
+
 int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
                          int64_t ld_y, const double* sos, int S, int clip, int64_t chunk_len,
                          const float* xs, int64_t n_in, int64_t ld_xs, int K, int L, int M,

@@ -124,7 +124,10 @@ __device__ __forceinline__ void emit_states(const float* s_out, double* scratch,
   {
     const int j = tid & (kWave - 1);
     const int grp = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (j < NSUB) {
+#ifndef DSP_ST_EXP
+#define DSP_ST_EXP 0  // timing ablations: 1 no sub-chunk dot products, 2 no Horner steps
+#endif
+    if (j < NSUB && DSP_ST_EXP != 1) {
       const float* yy = s_out + j * (kStU + 4);
       const const_f64_ptr g = (const_f64_ptr)st.g + 4 * grp;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
@@ -159,7 +162,7 @@ __device__ __forceinline__ void emit_states(const float* s_out, double* scratch,
   const int64_t cs = ck * NJ;       // the chunk's first sub-chunk
   const int ja = (int)(max(cs, jt0) - jt0);
   const int jb = (int)min((int64_t)NSUB, cs + NJ - jt0);
-  const int steps = act ? (int)(cs + NJ - jt0) - ja : 0;
+  const int steps = act && DSP_ST_EXP != 2 ? (int)(cs + NJ - jt0) - ja : 0;
   const int ir = i < D ? i : 0;
   double arow[D];
 #pragma unroll

@@ -482,3 +482,26 @@ def test_chain_src_emitted_states(gpu, n_in, chunk_len):
         assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
         assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
         assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+
+
+def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
+    """x rows that are not 16-byte aligned (n_in % 4 != 0) cannot feed the
+    x-domain chunk states; the chain then uses the y-domain table (the
+    contract in include/dspcore.h) instead of failing, bitwise equal to the
+    staged path, and still matches the reference recipe."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    n_in = 47999
+    cfg = ChainConfig(n_in, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, 3, gpu)
+    gen = torch.Generator(device=gpu).manual_seed(13)
+    x = torch.rand((3, n_in), generator=gen, device=gpu) * 2 - 1
+    with _chain_mode(0):
+        y, z, mag = (t.clone() for t in ch.run(x))
+    y2, z2, m2 = ch.run_stages(x)
+    assert torch.equal(y, y2) and torch.equal(z, z2) and torch.equal(mag, m2)
+    for b in range(3):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, orc.CONFIG3_GAINS,
+                                       None, 4096)
+        assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
