@@ -1034,12 +1034,15 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const bool span_ok = n * 4 + 16 < (int64_t)kOob && (p1mode != 2 || XS.n * 4 + 16 < (int64_t)kOob);
   const int VMr = (vec_x && vec_y && span_ok) ? ((n % 4 == 0) ? 1 : 2) : 0;
   const dim3 grid((unsigned)B);
-  const int W = C <= kWave ? 1 : 4;
+  const int W = C <= kWave ? 1 : C <= 2 * kWave ? 2 : 4;
 #define DSP_WAVE_LAUNCH(P1v, VMv, NV)                                                         \
   do {                                                                                        \
     if (W == 1)                                                                               \
       hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV, 1>), grid, dim3(kWave), 0, s, x, y, B,  \
                          n, ld_x, ld_y, p, sp, G, T, C, clip, XS);                            \
+    else if (W == 2)                                                                          \
+      hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV, 2>), grid, dim3(2 * kWave), 0, s, x, y, \
+                         B, n, ld_x, ld_y, p, sp, G, T, C, clip, XS);                         \
     else                                                                                      \
       hipLaunchKernelGGL((k_iir_wave<S, P1v, VMv, NV, 4>), grid, dim3(4 * kWave), 0, s, x, y, \
                          B, n, ld_x, ld_y, p, sp, G, T, C, clip, XS);                         \

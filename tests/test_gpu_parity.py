@@ -153,6 +153,7 @@ def test_eq_chunk_carry_is_exact_to_rounding(gpu):
         "fused+table, 1 wave, 63 chunks": dict(chunk_len=1152),
         "fused, 36 chunks": dict(chunk_len=2048),
         "fused 4 waves, 141 chunks": dict(chunk_len=512),
+        "fused 2 waves, 125 chunks": dict(chunk_len=576),
         "general, 282 chunks": dict(chunk_len=256),
     }
     for name, kw in variants.items():

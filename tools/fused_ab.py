@@ -19,7 +19,8 @@ cfg = ChainConfig(48000, 48000, L, M, None, gains, n_fft=4096)
 dev = torch.device("cuda", 0)
 x = torch.rand((B, 48000), device=dev, generator=torch.Generator(device=dev).manual_seed(0))
 x = x * 2 - 1
-ch = Chain(cfg, B, dev)
+T = int(os.environ.get("CHAIN_T", 0)) or None
+ch = Chain(cfg, B, dev, chunk_len=T)
 res = {}
 modes = [int(m) for m in os.environ.get("FUSION_MODES", "1,0").split(",")]
 for rnd in range(3):
@@ -36,6 +37,6 @@ for rnd in range(3):
         _lib.trace_enable(False)
         for k, ms in recs:
             res.setdefault((mode, k), []).append(ms)
-print(os.path.basename(_lib.LIB_PATH), f"L/M={L}/{M}",
+print(os.path.basename(_lib.LIB_PATH), f"L/M={L}/{M} T={ch.chunk_len}",
       {f"m{m}:{k}": round(float(np.median(v)), 4) for (m, k), v in res.items()},
       "z00", float(ch.z[0, 1000]))
