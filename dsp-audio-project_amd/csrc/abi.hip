@@ -22,10 +22,9 @@ struct TraceState {
   size_t used = 0;
 };
 thread_local TraceState g_trace;
-// dsp_chain_fusion: 0 x-domain chunk states (default), 1 fused SRC + cascade
-// launch, 2 chunk states emitted by the SRC kernel (1 and 2 measured slower,
-// DESIGN.md §3.5).
-thread_local int g_chain_mode = 0;
+// dsp_chain_path: 0 single-pass kernel where instantiated (default), 1 always
+// the two-launch chain.
+thread_local int g_chain_path = 0;
 }  // namespace
 
 TraceScope::TraceScope(const char* name, hipStream_t s) : slot_(-1), s_(s) {
@@ -132,17 +131,23 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_
                           window, twiddles, static_cast<hipStream_t>(stream));
 }
 
-int dsp_chain_fusion(int32_t mode) {
+int dsp_chain_path(int32_t path) {
   dsp::clear_error();
-  if (mode < -1 || mode > 2) return dsp::set_error(DSP_EINVAL, "chain mode %d not in [-1, 2]", mode);
-  const int prev = dsp::g_chain_mode;
-  if (mode >= 0) dsp::g_chain_mode = mode;
+  if (path < -1 || path > 1) return dsp::set_error(DSP_EINVAL, "chain path %d not in [-1, 1]", path);
+  const int prev = dsp::g_chain_path;
+  if (path >= 0) dsp::g_chain_path = path;
   return prev;
 }
 
-size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S, int64_t chunk_len) {
+int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,
+                           int64_t c_offset, int32_t S) {
+  return dsp::chain_tile_sub(n_in, n_out, K, L, M, c_offset, S);
+}
+
+size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t K, int32_t L,
+                                 int32_t M, int64_t c_offset, int32_t S, int64_t chunk_len) {
   const size_t a = dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
-  const size_t b = (2 * S == dsp::kStD) ? dsp::chain_states_bytes(B, n_out, chunk_len) : 0;
+  const size_t b = dsp::chain_tile_workspace_bytes(B, n_in, n_out, K, L, M, c_offset, S);
   return a > b ? a : b;
 }
 
@@ -166,27 +171,22 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
   if (B == 0) return DSP_OK;
   int rc = dsp::kNotFused;
-  if (xstate_table && S > 0 && dsp::g_chain_mode == 1)
-    rc = dsp::launch_chain_fused(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
-                                 sos_host, S, clip, chunk_len, xstate_table, xstate_rows, s);
-  else if (S > 0 && dsp::g_chain_mode == 2)
-    rc = dsp::launch_chain_ystate(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
-                                  sos_host, S, clip, chunk_len, state_table, workspace,
-                                  workspace_bytes, s);
-  if (rc == DSP_OK)
-    return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
-                                twiddles, s);
-  if (rc != dsp::kNotFused) return rc;
-  rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
-  if (rc) return rc;
-  // The x-domain states need aligned input rows and a fitting chunking;
-  // otherwise the y-domain table serves (include/dspcore.h).
-  if (xstate_table && dsp::xstate_applicable(n_out, S, chunk_len, x, ld_x, L, M))
-    rc = dsp::launch_biquad_xstate(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len, x,
-                                   n_in, ld_x, K, L, M, c_offset, xstate_table, xstate_rows, s);
-  else
-    rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
-                            state_table, workspace, workspace_bytes, s);
+  if (dsp::g_chain_path == 0)
+    rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
+                                sos_host, S, clip, workspace, workspace_bytes, s);
+  if (rc == dsp::kNotFused) {
+    // Two-launch chain: SRC, then the cascade with x-domain chunk states where
+    // the input rows are aligned and the chunking fits, else the y-domain
+    // table (include/dspcore.h).
+    rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
+    if (rc) return rc;
+    if (xstate_table && dsp::xstate_applicable(n_out, S, chunk_len, x, ld_x, L, M))
+      rc = dsp::launch_biquad_xstate(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len, x,
+                                     n_in, ld_x, K, L, M, c_offset, xstate_table, xstate_rows, s);
+    else
+      rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
+                              state_table, workspace, workspace_bytes, s);
+  }
   if (rc) return rc;
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
                               twiddles, s);

@@ -1,0 +1,460 @@
+// Single-pass SRC -> biquad cascade, the default path of dsp_chain_f32 (gfx950).
+//
+// Replaces, for a batch of channels, reference app.py:164-167:
+//   y = conversion_tasa_muestreo(x, fs, M, L)   modules/dsp_core.py:133-173
+//   z = sistema_ecualizador(y, fs', gains)      modules/dsp_core.py:216-254
+// in ONE launch that reads x once and writes y and z once: HBM traffic is the
+// algorithmic 4*N_in + 8*N_out bytes per channel, against 4*N_in + 4*N_out
+// (SRC kernel) + 4*N_in*rows/shift + 8*N_out (two-pass cascade) for the
+// two-launch chain.
+//
+// Decomposition.  A workgroup is ONE wavefront and owns a tile of 64*TSUB
+// consecutive outputs of one channel; lane l owns the sub-chunk of TSUB
+// outputs l*TSUB .. l*TSUB + TSUB-1 of the tile, TSUB = 32*L/M, i.e. exactly
+// 32 new input samples per lane.  Because TSUB*M is a multiple of L, every
+// lane (and every tile) sees the same polyphase pattern: output i of a
+// sub-chunk reads x[32*l + qi(i) - t] with branch phi(i) (compile-time), so
+// the taps are wave-uniform (scalar loads) and each lane runs
+//   1. SRC: y[i] = sum_u P[phi(i)][TT-1-u] * w[qi(i) + u] from its 72-sample
+//      window, read from the tile's x window in LDS (one coalesced load per
+//      tile, padded so the 64 lanes' ds_read_b128 are conflict-free).  Same
+//      per-output FMA order as k_src_reg: y is bitwise the SRC kernel's.
+//   2. pass 1: the sub-chunk's zero-state end state E_l: the cascade run over
+//      the lane's TSUB outputs from zero state (float64).
+//   3. carry: the tile's entry state S_in comes from the previous tile of the
+//      same channel (chained hand-off, below); 12 lanes run the serial scan
+//      S_{l+1} = A^TSUB S_l + E_l over the 64 sub-chunks in LDS, float64.
+//   4. the tile's end state S_64 is published for the next tile;
+//   5. y leaves through LDS as coalesced float4 stores; pass 2 reruns the
+//      cascade over the lane's sub-chunk from S_l, clips, and z leaves the
+//      same way.
+// y never returns from HBM, and there is no second pass over x.
+//
+// Chained hand-off.  Workgroups are numbered tile-major (id = tile*B + b), so
+// tile t-1 of a channel was dispatched B workgroups before tile t; at B >= the
+// chip's resident wave count its end state is normally published long before
+// tile t needs it.  A workgroup waits only on a lower id, and ids are
+// dispatched in order, so every wait ends.  The state (12 doubles) and its
+// flag follow the agent-scope hand-off the gfx950 guide measures valid: the
+// producer's lanes store the payload with sc1 stores, wait vmcnt(0), then one
+// lane stores the flag sc1; the consumer polls the flag with sc1 loads and then
+// loads the payload with sc1 loads.  The consumer clears the flag, so a
+// completed launch leaves the flag array zero for the next one (the caller
+// zero-fills the workspace once).  A wait that exceeds ~1 s (a broken dispatch
+// order) gives up, marks the workspace's error word and continues: no hang.
+//
+// Rows are bitwise independent of the batch size: the geometry depends on
+// (L, M, K) only.
+#include "cascade.h"
+
+namespace dsp {
+namespace {
+
+constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
+constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
+constexpr int kD = 2 * kS;
+constexpr uint32_t kMaxSpins = 1u << 23;  // x s_sleep 2 (128 clk): ~0.4 s
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Padded LDS image of the tile's x window: 4 floats after every 32, so lane l's
+// window (x offset 32 l) starts at float 36 l; the 64 lanes' ds_read_b128 then
+// cover all 64 banks once per lane group and are 16-byte aligned.
+__host__ __device__ constexpr int xpad(int g) { return g + 4 * (g >> 5); }
+
+template <int L_, int M_, int TT_, int CR_>
+struct TileGeo {
+  static constexpr int L = L_, M = M_, TT = TT_, CR = CR_;
+  static_assert((kLS * L) % M == 0, "32 input samples per sub-chunk must make whole outputs");
+  static constexpr int TSUB = kLS * L / M;   // outputs per lane
+  static constexpr int TILE = kWave * TSUB;  // outputs per workgroup
+  static_assert(TSUB % 8 == 0 && TSUB <= kWave, "two float4 halves; prep lanes");
+  static constexpr int qi(int i) { return (i * M + CR) / L; }
+  static constexpr int phi(int i) { return (i * M + CR) % L; }
+  static constexpr int W = qi(TSUB - 1) + TT;                       // lane window
+  static constexpr int NWIN = (kLS * (kWave - 1) + W + 3) / 4 * 4;  // tile window
+  static constexpr int XF = xpad(NWIN + 4) + 4;                     // x image (floats)
+  static constexpr int RS = TSUB + 4;                               // staging row stride
+  static constexpr int SF = (kWave / 2) * RS;                       // staging (floats)
+  static constexpr int CF = (kWave + 1) * kD * 2;                   // scan slots (floats)
+  static constexpr int LDSF = XF > SF ? (XF > CF ? XF : CF) : (SF > CF ? SF : CF);
+  static constexpr int TB = TT * 4;  // tap bank: [u][phase], phase padded to 4
+  static_assert(L <= 4, "one float4 of taps per tap index");
+};
+
+struct TileArgs {
+  const float* x;
+  float* y;
+  float* z;
+  const float* taps;  // float32 L*h[K]
+  const double* P;    // A^TSUB [12][12] in the workspace (k_tile_prep)
+  double* states;     // [B][ntiles][12] tile end states
+  uint32_t* flags;    // [B][ntiles]
+  uint32_t* err;      // set when a hand-off wait gave up
+  int64_t B, n_in, ld_x, n_out, ld_y, ntiles, cq;
+  int K, clip;
+  SosParams p;
+};
+
+// Host -> workspace copy of A^TSUB (kernel argument of k_tile_prep).
+struct PMat {
+  double v[kD * kD];
+};
+
+__device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
+
+// Pins v[0..N) at this point of the program: the values are computed before it
+// and later uses start after it.  Keeps the scheduler from overlapping phases
+// whose live registers together exceed the 128 VGPRs of 4 waves per SIMD.
+template <int N, class T>
+__device__ __forceinline__ void pin(T (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+// Agent-scope hand-off accesses: global (never flat) loads/stores with sc1.
+__device__ __forceinline__ uint32_t load_flag(const uint32_t* p) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)p,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_flag(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)p, v,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_state(const double* p) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) double*)p,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_state(double* p, double v) {
+  __hip_atomic_store((__attribute__((address_space(1))) double*)p, v,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// SRC outputs H0 .. H0+NH-1 of the lane's sub-chunk from its window at xw
+// (padded LDS image).  Per output: u ascending from 0, fmaf(tap, x, acc) --
+// k_src_reg's order, so the float32 results are bitwise the same.
+template <class GEO, int H0, int NH>
+__device__ __forceinline__ void src_part(const float* xw, const float* bank,
+                                         float (&y)[GEO::TSUB]) {
+  constexpr int V0 = GEO::qi(H0) / 4 * 4;
+  constexpr int V1 = GEO::qi(H0 + NH - 1) + GEO::TT;
+  constexpr int NV = (V1 - V0 + 3) / 4 * 4;
+  float w[NV];
+#pragma unroll
+  for (int k = 0; k < NV / 4; ++k) {
+    const int v = V0 + 4 * k;
+    const float4 f = *reinterpret_cast<const float4*>(xw + xpad(v));
+    w[4 * k + 0] = f.x;
+    w[4 * k + 1] = f.y;
+    w[4 * k + 2] = f.z;
+    w[4 * k + 3] = f.w;
+  }
+  float acc[NH];
+#pragma unroll
+  for (int i = 0; i < NH; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int u = 0; u < GEO::TT; ++u) {
+    const float4 t4 = *reinterpret_cast<const float4*>(bank + 4 * u);  // broadcast
+    const float tp[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int i = 0; i < NH; ++i)
+      acc[i] = fmaf(tp[GEO::phi(H0 + i)], w[GEO::qi(H0 + i) - V0 + u], acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NH; ++i) y[H0 + i] = acc[i];
+}
+
+// Stores the tile's 64 x TSUB outputs (lane l holds outputs l*TSUB + i) as
+// coalesced float4s: each half of the lanes writes its rows into LDS (row
+// stride TSUB + 4: conflict-free ds_write_b128), then all 64 lanes store the
+// half's contiguous 32*TSUB floats.  Stores past the row's end are dropped by
+// the buffer resource.
+template <class GEO>
+__device__ __forceinline__ void store_tile(float* lds, const float (&v)[GEO::TSUB], int lane,
+                                           __amdgpu_buffer_rsrc_t rs, int64_t m0) {
+  constexpr int TS = GEO::TSUB, RS = GEO::RS;
+  constexpr int NF4 = (kWave / 2) * TS / 4;
+  static_assert(NF4 % kWave == 0, "whole float4 rounds per half");
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    fence();
+    if ((lane >> 5) == h) {
+      float* row = lds + (lane & 31) * RS;
+#pragma unroll
+      for (int k = 0; k < TS / 4; ++k)
+        *reinterpret_cast<float4*>(row + 4 * k) =
+            make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    fence();
+#pragma unroll
+    for (int k = 0; k < NF4 / kWave; ++k) {
+      const int g = 4 * (lane + kWave * k);
+      const int r = g / TS, c = g - r * TS;
+      const float4 f = *reinterpret_cast<const float4*>(lds + r * RS + c);
+      u32x4 d;
+      d.x = __float_as_uint(f.x);
+      d.y = __float_as_uint(f.y);
+      d.z = __float_as_uint(f.z);
+      d.w = __float_as_uint(f.w);
+      const int64_t off = (m0 + (int64_t)h * (kWave / 2) * TS + g) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, 0);
+    }
+  }
+  fence();
+}
+
+template <class GEO>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
+    TileArgs a) {
+  constexpr int TS = GEO::TSUB;
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  __shared__ __attribute__((aligned(16))) float bank[GEO::TB];
+  const int lane = threadIdx.x;
+  const int64_t id = blockIdx.x;
+  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
+  const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
+
+  // ---- tap bank: bank[u][ph] = taps[ph + L*(TT-1-u)] (0 past K): tap u of
+  // branch ph in the reversed order the SRC sums in.
+  for (int i = lane; i < GEO::TB; i += kWave) {
+    const int u = i >> 2, ph = i & 3, k = ph + GEO::L * (GEO::TT - 1 - u);
+    bank[i] = (ph < GEO::L && k < a.K) ? a.taps[k] : 0.f;
+  }
+  // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);  // multiple of 4
+    constexpr int NF = GEO::NWIN / 4;
+#pragma unroll
+    for (int k = 0; k < (NF + kWave - 1) / kWave; ++k) {
+      const int f = lane + kWave * k;
+      if ((k + 1) * kWave <= NF || f < NF) {
+        // "Negative" offsets (tile 0) are >= 2^31 as unsigned: out of range, zeros.
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, 0);
+        *reinterpret_cast<float4*>(lds + xpad(4 * f)) = make_float4(v.x, v.y, v.z, v.w);
+      }
+    }
+  }
+  fence();  // one wave: its LDS operations execute in order
+
+  // ---- 1. SRC: the lane's TSUB outputs, in two halves (register pressure)
+  float y[TS];
+  {
+    const float* xw = lds + 36 * lane;
+    src_part<GEO, 0, TS / 2>(xw, bank, y);
+    pin(y);
+    fence();
+    src_part<GEO, TS / 2, TS / 2>(xw, bank, y);
+    pin(y);
+  }
+
+  // ---- 2. pass 1: zero-state end state of the sub-chunk
+  double e[kD];
+  {
+    double w1[kS], w2[kS];
+#pragma unroll
+    for (int k = 0; k < kS; ++k) w1[k] = w2[k] = 0.0;
+#pragma unroll
+    for (int i = 0; i < TS; ++i) (void)cascade_step<kS, true>((double)y[i], w1, w2, a.p);
+#pragma unroll
+    for (int k = 0; k < kS; ++k) {
+      e[2 * k] = w1[k];
+      e[2 * k + 1] = w2[k];
+    }
+  }
+  // Keep the SRC and pass 1 ahead of the hand-off wait (the compiler would
+  // otherwise sink them past it).
+  pin(e);
+
+  // ---- 3. entry state of the tile, then the carry scan over the sub-chunks
+  double s_in = 0.0;
+  if (tile > 0) {
+    const int64_t prev = b * a.ntiles + tile - 1;
+    if (lane == 0) {
+      uint32_t spins = 0;
+      while (load_flag(a.flags + prev) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == kMaxSpins) {
+          store_flag(a.err, 1u);
+          break;
+        }
+      }
+    }
+    fence();
+    if (lane < kD) s_in = load_state(a.states + prev * kD + lane);
+    if (lane == 0) store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
+  }
+  fence();
+  double* sc = reinterpret_cast<double*>(lds);  // slot j = S_j (j = 0..64)
+#pragma unroll
+  for (int d = 0; d < kD; ++d) sc[(1 + lane) * kD + d] = e[d];
+  if (lane < kD) sc[lane] = s_in;
+  fence();
+  if (lane < kD) {
+    double prow[kD];
+#pragma unroll
+    for (int j = 0; j < kD; ++j) prow[j] = a.P[lane * kD + j];  // lane-varying: vector loads
+    for (int cc = 0; cc < kWave; ++cc) {
+      const double* s = sc + cc * kD;
+      double a0 = sc[(1 + cc) * kD + lane], a1 = 0.0, a2 = 0.0;
+#pragma unroll
+      for (int j = 0; j < kD; j += 3) {
+        a0 = fma(prow[j], s[j], a0);
+        a1 = fma(prow[j + 1], s[j + 1], a1);
+        a2 = fma(prow[j + 2], s[j + 2], a2);
+      }
+      fence();  // every lane's reads of S_cc precede the write
+      sc[(1 + cc) * kD + lane] = (a0 + a1) + a2;
+      fence();
+    }
+  }
+  fence();
+
+  // ---- 4. publish the tile's end state for the next tile of the channel
+  if (tile + 1 < a.ntiles) {
+    const int64_t me = b * a.ntiles + tile;
+    if (lane < kD) store_state(a.states + me * kD + lane, sc[kWave * kD + lane]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) store_flag(a.flags + me, 1u);
+  }
+
+  double s1[kS], s2[kS];
+#pragma unroll
+  for (int k = 0; k < kS; ++k) {
+    s1[k] = sc[lane * kD + 2 * k];
+    s2[k] = sc[lane * kD + 2 * k + 1];
+  }
+  fence();
+
+  // ---- 5. y out, pass 2, z out
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+  store_tile<GEO>(lds, y, lane, ry, m0);
+  pin(y);
+  const float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+#pragma unroll
+  for (int i = 0; i < TS; ++i)
+    y[i] = clip_f32((float)cascade_step<kS, true>((double)y[i], s1, s2, a.p), lo, hi);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+      a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+  store_tile<GEO>(lds, y, lane, rz, m0);
+}
+
+// A^TSUB (computed on the host in float64) into the workspace, where the scan
+// lanes read their rows with vector loads.
+__global__ __launch_bounds__(kWave) void k_tile_prep(PMat m, double* P) {
+  for (int i = threadIdx.x; i < kD * kD; i += kWave) P[i] = m.v[i];
+}
+
+// Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
+// benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
+typedef TileGeo<3, 2, 41, 0> Geo3241;
+
+struct TilePlan {
+  int64_t tsub, tile, ntiles;
+};
+
+bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
+                   TilePlan* tp) {
+  const int TT = (K + L - 1) / L;
+  if (!(L == 3 && M == 2 && TT == 41 && c % L == 0)) return false;
+  if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || n_out % 4) return false;
+  if (n_in * 4 + 16 >= ((int64_t)1 << 31) || n_out * 4 + 16 >= ((int64_t)1 << 31)) return false;
+  // Lane windows on 16-byte boundaries: x offset of tile t's window is
+  // t*2048 + c/L - (TT-1), a multiple of 4 iff c/L - (TT-1) is.
+  if (((c / L) - (TT - 1)) % 4 != 0) return false;
+  tp->tsub = Geo3241::TSUB;
+  tp->tile = Geo3241::TILE;
+  tp->ntiles = ceil_div(n_out, tp->tile);
+  return true;
+}
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct TileWs {
+  size_t err_off, g_off, st_off, fl_off, total;
+};
+
+TileWs tile_ws(int64_t B, int64_t ntiles, int64_t tsub) {
+  TileWs w;
+  w.err_off = 0;  // include/dspcore.h: the workspace's first word
+  w.g_off = 256;  // A^TSUB
+  w.st_off = w.g_off + align256((size_t)kD * kD * sizeof(double));
+  w.fl_off = w.st_off + align256((size_t)B * ntiles * kD * sizeof(double));
+  w.total = w.fl_off + align256((size_t)B * ntiles * sizeof(uint32_t));
+  return w;
+}
+
+}  // namespace
+
+int64_t chain_tile_sub(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S) {
+  TilePlan tp;
+  return tile_geometry(n_in, n_out, K, L, M, c, S, &tp) ? tp.tsub : 0;
+}
+
+size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M,
+                                  int64_t c, int S) {
+  TilePlan tp;
+  if (B <= 0 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 0;
+  return tile_ws(B, tp.ntiles, tp.tsub).total;
+}
+
+int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
+                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
+                      int64_t c, const double* sos, int S, int clip, void* ws, size_t ws_bytes,
+                      hipStream_t s) {
+  TilePlan tp;
+  if (!tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
+  auto aligned = [](const void* p, int64_t ld) {
+    return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  };
+  if (!aligned(x, ld_x) || !aligned(y, ld_y) || !aligned(z, ld_y)) return kNotFused;
+  SosParams p;
+  if (S > 0 && !realize(sos, S, &p)) return kNotFused;  // a b0 == 0 band: no NORM form
+  if (S == 0) realize(nullptr, 0, &p);
+  const TileWs w = tile_ws(B, tp.ntiles, tp.tsub);
+  DSP_REQUIRE(ws && ws_bytes >= w.total, "chain workspace too small: %zu < %zu bytes", ws_bytes,
+              w.total);
+  DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 255) == 0, "chain workspace not 256-B aligned");
+  DSP_REQUIRE(B * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
+  char* base = static_cast<char*>(ws);
+  TileArgs a;
+  a.x = x;
+  a.y = y;
+  a.z = z;
+  a.taps = taps;
+  a.P = reinterpret_cast<const double*>(base + w.g_off);
+  a.states = reinterpret_cast<double*>(base + w.st_off);
+  a.flags = reinterpret_cast<uint32_t*>(base + w.fl_off);
+  a.err = reinterpret_cast<uint32_t*>(base + w.err_off);
+  a.B = B;
+  a.n_in = n_in;
+  a.ld_x = ld_x;
+  a.n_out = n_out;
+  a.ld_y = ld_y;
+  a.ntiles = tp.ntiles;
+  a.cq = c / L;
+  a.K = K;
+  a.clip = clip;
+  a.p = p;
+  PMat pm;
+  const std::vector<double> P = chunk_transition(p, kS, tp.tsub);
+  for (int i = 0; i < kD * kD; ++i) pm.v[i] = P[i];
+  {
+    TraceScope trace("chain_prep", s);
+    hipLaunchKernelGGL(k_tile_prep, dim3(1), dim3(kWave), 0, s, pm,
+                       reinterpret_cast<double*>(base + w.g_off));
+  }
+  DSP_LAUNCHED("k_tile_prep");
+  {
+    TraceScope trace("chain_tile", s);
+    hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,
+                       a);
+  }
+  DSP_LAUNCHED("k_chain_tile");
+  return DSP_OK;
+}
+
+}  // namespace dsp

@@ -96,38 +96,6 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 
-// Chain mode 2 (dsp_chain_fusion): the SRC kernel emits the cascade's chunk end
-// states from the y tile it already holds in LDS, so the cascade skips its
-// first pass.  A tile of TILE outputs is cut into sub-chunks of kStU samples;
-// sub-chunk j's zero-state end state is s_j = sum_t g[t] y[kStU*j + t] with
-// g[t] = A^(kStU-1-t) b (the last kStU rows of the y-domain state table G of
-// chunk_len), and every chunk piece the tile holds is carried to the chunk's
-// end by Horner steps S <- A^kStU S + s_j.  A chunk overlaps at most two tiles
-// (chunk_len <= TILE): part[b][c][slot][kStD], slot = tile - first tile of c,
-// and the cascade sums the two slots in that order (deterministic).
-constexpr int kStU = 96;       // sub-chunk length
-constexpr int kStD = 12;       // state dimension (S = 6 stages)
-constexpr int kStPieces = 12;  // chunk pieces per tile (16 lanes each, 192 threads)
-struct SrcStates {
-  double* part;             // [B][C][2][kStD]
-  const double* g;          // [kStU][kStD], device
-  double AU[kStD * kStD];   // A^kStU, row-major
-  int64_t chunk_len;
-  int C;
-};
-// SRC with state emission; kNotFused (nothing launched) unless the geometry
-// is instantiated ((L, M, ceil(K/L)) = (3, 2, 41)).
-int launch_src_states(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
-                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
-                      int64_t c, const SrcStates& st, hipStream_t s);
-int src_states_tile(int L, int M, int K);  // TILE of that instantiation, 0 if none
-size_t chain_states_bytes(int64_t B, int64_t n_out, int64_t chunk_len);
-// SRC (emitting states) + cascade reading them; kNotFused if not applicable.
-int launch_chain_ystate(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
-                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
-                        int L, int M, int64_t c, const double* sos, int S, int clip,
-                        int64_t chunk_len, const double* state_table, void* ws,
-                        size_t ws_bytes, hipStream_t s);
 // Audio I/O (audio_io.hip).
 int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames);
@@ -142,12 +110,16 @@ int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, in
 // the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
                     int64_t* q0, int64_t* rows);
-// Fused SRC + cascade (one launch, y never re-read).  Returns kNotFused, with
-// nothing launched, when the geometry has no instantiation.
-int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
-                       int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
-                       int L, int M, int64_t c, const double* sos, int S, int clip,
-                       int64_t chunk_len, const double* gx, int64_t gx_rows, hipStream_t s);
+// Single-pass chain (chain_tile.hip): y = SRC(x) and z = clip(cascade(y)) in
+// one launch, y never re-read.  chain_tile_sub returns the sub-chunk length of
+// the instantiated geometry (0: the two-launch chain serves this call).
+int64_t chain_tile_sub(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S);
+size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M,
+                                  int64_t c, int S);
+int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
+                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
+                      int64_t c, const double* sos, int S, int clip, void* ws, size_t ws_bytes,
+                      hipStream_t s);
 // Whether launch_biquad_xstate's conditions on the cascade (n, S, chunk_len)
 // and on the SRC input rows (16-byte aligned) hold.
 bool xstate_applicable(int64_t n, int S, int64_t chunk_len, const float* xs, int64_t ld_xs,

@@ -48,48 +48,11 @@
 #include <cmath>
 #include <vector>
 
-#include "common.h"
+#include "cascade.h"
 
 namespace dsp {
 namespace {
 
-// Direct form II realisation: c[k] = {g, c1, c2, a1, a2} and input gain G.
-// NORM (every b0 != 0): g = 1, c1 = b1/b0, c2 = b2/b0, G = prod b0.
-// Otherwise: g = b0, c1 = b1, c2 = b2, G = 1.  Stages past S are identities.
-struct SosParams {
-  double c[DSP_MAX_STAGES][5];
-  double G;
-};
-
-// Host: realisation of a [S][5] {b0 b1 b2 a1 a2} cascade; returns NORM.  Must
-// match dspcore/design.py:df2_realization, which builds the state tables.
-bool realize(const double* sos, int S, SosParams* p) {
-  bool norm = true;
-  for (int k = 0; k < S; ++k) norm = norm && sos[5 * k] != 0.0;
-  p->G = 1.0;
-  for (int k = 0; k < DSP_MAX_STAGES; ++k) {
-    double* c = p->c[k];
-    if (k >= S) {
-      c[0] = 1.0;
-      c[1] = c[2] = c[3] = c[4] = 0.0;
-      continue;
-    }
-    const double* r = sos + 5 * k;
-    if (norm) {
-      c[0] = 1.0;
-      c[1] = r[1] / r[0];
-      c[2] = r[2] / r[0];
-      p->G *= r[0];
-    } else {
-      c[0] = r[0];
-      c[1] = r[1];
-      c[2] = r[2];
-    }
-    c[3] = r[3];
-    c[4] = r[4];
-  }
-  return norm;
-}
 struct ScanParams {
   double P[16 * 16];  // A^T, row-major D x D, D = 2S <= 16
 };
@@ -99,40 +62,6 @@ constexpr int kTS = 32;        // samples per tile step (chunk_len granule)
 constexpr int kRow = kTS + 1;  // LDS row stride in floats
 constexpr int kLoads = kTS / 4;  // float4 loads per thread per tile (one row per thread)
 constexpr int kCBMax = 4 * kWave;  // max chunks per channel in the fused kernel
-#ifndef DSP_CHAIN_EXP
-#define DSP_CHAIN_EXP 0  // fused chain timing ablations: 1 no SRC FMAs, 2 no cascade, 3 no y/z stores,
-                         // 4/5 32 of NOUT outputs stored at 128-B aligned / NOUT-strided offsets
-#endif
-#ifndef DSP_IIR_EXPERIMENT
-#define DSP_IIR_EXPERIMENT 0  // 1: no arithmetic, 2: no global loads (timing only)
-#endif
-
-// One sample through the S-stage cascade; w1/w2 are the stages' delay lines.
-template <int S, bool NORM>
-__device__ __forceinline__ double cascade_step(double u, double (&w1)[S > 0 ? S : 1],
-                                               double (&w2)[S > 0 ? S : 1],
-                                               const SosParams& p) {
-  if constexpr (NORM && S > 0) u *= p.G;
-#pragma unroll
-  for (int k = 0; k < S; ++k) {
-    const double w = fma(-p.c[k][4], w2[k], fma(-p.c[k][3], w1[k], u));
-    const double h = NORM ? w : p.c[k][0] * w;
-    u = fma(p.c[k][2], w2[k], fma(p.c[k][1], w1[k], h));
-    w2[k] = w1[k];
-    w1[k] = w;
-  }
-  return u;
-}
-
-// np.clip(v, lo, hi) with NaN kept (v_med3_f32 maps NaN to a bound).
-// Clipping after the float32 rounding gives the same result as rounding the
-// float64 clip (|v| <= 1 rounds to |v| <= 1, anything beyond rounds to
-// beyond-or-equal).  lo/hi = -inf/+inf is the identity.
-__device__ __forceinline__ float clip_f32(float v, float lo, float hi) {
-  const float m = __builtin_amdgcn_fmed3f(v, lo, hi);
-  return v != v ? v : m;
-}
-
 // Row descriptors live in LDS: global offset of the row's first sample for
 // input and output, and the valid sample range [lo, len) of the row.
 struct Rows {
@@ -342,13 +271,8 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
   float* my = tile + tid * kRow;
   float4 v[kLoads];
   tile_sync<NR>();  // every thread's row descriptors are written
-#if DSP_IIR_EXPERIMENT == 2 || DSP_IIR_EXPERIMENT == 4
-#pragma unroll
-  for (int i = 0; i < kLoads; ++i) v[i] = make_float4(0.25f, -0.5f, 0.125f, 0.75f);
-#else
   if constexpr (AFF) fetch_aff(v, io, 0);
   else fetch<NR, VIN>(v, x, rows, 0, tid);
-#endif
   // Tiles in [span_lo, span_hi) lie inside the range of every row of the wave
   // that has one and are put unmasked (a row without samples is a chunk whose
   // state is never used).  Pass 2 never masks: outputs past a row's end are
@@ -373,20 +297,11 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
     else
       tile_put<NR, true>(tile, v, rows, t0, tid);
     tile_sync<NR>();
-#if DSP_IIR_EXPERIMENT != 2 && DSP_IIR_EXPERIMENT != 4
     if (t0 + kTS < (int)T) {
       if constexpr (AFF) fetch_aff(v, io, t0 + kTS);
       else fetch<NR, VIN>(v, x, rows, t0 + kTS, tid);
     }
-#endif
-#if DSP_IIR_EXPERIMENT == 1
-    if (MODE == kStateTable) e[0] += my[3];
-    if constexpr (MODE == kApply) {
-      if (clip == 12345) my[0] = 1.f;
-    } else if constexpr (false) {
-#else
     if constexpr (MODE == kStateTable) {
-#endif
       const double* g = G + t0 * D;
 #pragma unroll 4
       for (int j = 0; j < kTS; ++j) {
@@ -403,9 +318,6 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
     }
     if constexpr (MODE == kApply) {
       tile_sync<NR>();
-#if DSP_IIR_EXPERIMENT == 3 || DSP_IIR_EXPERIMENT == 4
-      if (clip == 12345)
-#endif
       if constexpr (AFF) store_aff<VM>(rsrc, tile, io, t0, tid);
       else tile_store<NR, VM>(y, rsrc, tile, rows, t0, tid);
     }
@@ -425,14 +337,9 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 // (dspcore/design.py:xstate_table).  Pass 1 then reads the SRC input (2/3 of
 // the bytes at L/M = 3/2) and costs 2S*M/L FMAs per output sample instead of
 // 2S, and the chunk states are those of the exact float64 SRC output.
-// P1 = 3 (chain mode 2): the end states come from the SRC kernel, two pieces
-// per chunk (common.h SrcStates): part[b][c][slot][2S], slot 1 present when the
-// chunk reaches into the SRC tile after the one holding its start.
 struct XState {
   const float* xs;  // SRC input rows [B][ld]
   int64_t ld, n, shift, q0, rows;
-  const double* part;  // P1 = 3
-  int64_t tile;        // P1 = 3: SRC tile length
 };
 
 // Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
@@ -557,22 +464,7 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
 
   // ---- pass 1: zero-state end state of the lane's chunk
   constexpr bool AFF = VM > 0;
-  static_assert(P1 != 3 || D == kStD, "SRC-emitted states are 12-dimensional");
-  if constexpr (P1 == 3) {
-    // Emitted by the SRC kernel: slot 0 from the tile holding the chunk's
-    // start, slot 1 from the next tile if the chunk reaches into it; summed in
-    // that order.
-    if (c + 1 < C) {
-      const double* e0 = XS.part + (b * C + c) * 2 * D;
-      const bool two = t_begin / XS.tile != (t_begin + T - 1) / XS.tile;
-#pragma unroll
-      for (int i = 0; i < D; ++i) e[i] = e0[i];
-      if (two) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) e[i] += e0[D + i];
-      }
-    }
-  } else if constexpr (P1 == 2) {
+  if constexpr (P1 == 2) {
     run_pass<S, kStateTable, kWave, VM, true, NORM, AFF>(XS.xs, y, rsrc, tile, rows, io1,
                                                          XS.rows, lane, s1, s2, e, p, G, clip);
   } else if constexpr (P1 == 1) {
@@ -598,211 +490,6 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
   // ---- pass 2: outputs from the carried state
   run_pass<S, kApply, kWave, VM, (VM > 0), NORM, AFF>(x, y, rsrc, tile, rows, io2, T, lane, s1,
                                                       s2, e, p, G, clip);
-}
-
-// ---------------------------------------------------------------------------
-// Fused SRC + cascade (chain fast path, dsp_chain_f32): ONE launch computes
-// y = SRC(x) and z = clip(EQ(y)) for a channel per wavefront without ever
-// reading y back from HBM.  Pass 1 and the carry scan are those of
-// k_iir_wave<P1 = 2> (chunk states straight from x); pass 2 then recomputes
-// the chunk's SRC outputs from x in registers, stores them (the drop-in API
-// returns y), runs the cascade on them and stores z.  HBM traffic per channel:
-// x twice (pass 1's overlapping rows, pass 2) + y + z, against x + y (SRC
-// kernel) + x + y + z (cascade) for the two-launch chain.
-//
-// SRC geometry for a compile-time (L, M, TT = ceil(K/L), BQ = c mod L):
-// lane c owns outputs m = c*T + t.  A pass-2 tile is NOUT = 32*L/M outputs,
-// i.e. exactly 32 new input samples, so every tile has the same phase pattern:
-// output i of tile k reads x[c*T*M/L + 32k + a + q(i) - u] (a = c div L,
-// q(i) = (i*M + BQ) div L) with the taps P[phi(i)][u], phi(i) = (i*M+BQ) mod L.
-// The lane keeps the window of WL = q(NOUT-1) + TT samples in registers: the
-// last CR = WL - 32 carry over, 32 new ones come from the coalesced x tile in
-// LDS.  Accumulation is one fmaf chain per output over the reversed taps, i.e.
-// k_src_reg's scalar order (DSP_SRC_PACK=0); the default SRC kernel pairs taps
-// in v_pk_fma_f32, so y agrees with it to float32 rounding.
-// ---------------------------------------------------------------------------
-template <int L_, int M_, int TT_, int BQ_>
-struct SrcGeo {
-  static constexpr int L = L_, M = M_, TT = TT_, BQ = BQ_;
-  static_assert((kTS * L) % M == 0, "32 input samples must make whole outputs");
-  static_assert(L <= 4, "one float4 of taps per tap index");
-  static constexpr int NOUT = kTS * L / M;  // outputs per tile
-  static_assert(NOUT % 4 == 0, "float4 stores");
-  static constexpr int q(int i) { return (i * M + BQ) / L; }
-  static constexpr int phi(int i) { return (i * M + BQ) % L; }
-  static constexpr int WL = q(NOUT - 1) + TT;  // window (input samples)
-  static constexpr int CR = WL - kTS;          // carried between tiles
-  static_assert(CR >= 0, "window shorter than a tile");
-  static constexpr int PRO = (CR + kTS - 1) / kTS;  // prologue tiles
-  static constexpr int OROW = NOUT + 1;        // LDS row stride of the y/z tile (odd)
-};
-
-// Pass-2 inputs of the fused kernel.
-struct FusedSrc {
-  float* y;            // SRC output rows (pitch = z's)
-  const float* taps;   // float32 L*h[K] (dsp_core.py:162)
-  int K;
-  int64_t nb0;         // channel-relative x index of chunk 0's first prologue block
-};
-
-// Stores the wave's 64-row x NOUT-float tile (LDS row stride OROW) to the
-// rows' [t0, t0 + NOUT) ranges: consecutive lanes take consecutive float4s of
-// a row, so each instruction writes ~NOUT*4-byte contiguous runs.  The buffer
-// resource spans one channel's row; stores past its end are dropped.
-#if DSP_CHAIN_EXP == 4 || DSP_CHAIN_EXP == 5
-constexpr int kNstExp = 32;  // ablation: 32 of the NOUT outputs stored
-#else
-constexpr int kNstExp = 0;
-#endif
-template <class SG>
-__device__ __forceinline__ void store_rows(__amdgpu_buffer_rsrc_t rs, const float* tile,
-                                           int64_t T, int t0, int lane) {
-  constexpr int V = (kNstExp ? kNstExp : SG::NOUT) / 4;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int s = 0; s < V; ++s) {
-    const int e = s * kWave + lane;
-    const int row = e / V, c4 = (e - row * V) * 4;
-    const float* src = tile + row * SG::OROW + c4;
-    u32x4 d;
-    d.x = __float_as_uint(src[0]);
-    d.y = __float_as_uint(src[1]);
-    d.z = __float_as_uint(src[2]);
-    d.w = __float_as_uint(src[3]);
-    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(((int64_t)row * T + t0 + c4) * 4), 0, 0);
-  }
-}
-
-template <int S, class SG>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2))) void k_chain_wave(
-    float* __restrict__ z, int64_t n, int64_t ld, SosParams p, ScanParams sp,
-    const double* __restrict__ G, int64_t T, int C, int clip, XState XS, FusedSrc FS) {
-  constexpr int D = 2 * S;
-  constexpr int NOUT = SG::NOUT, WL = SG::WL, CR = SG::CR, PRO = SG::PRO;
-  constexpr int TILE = (kWave * SG::OROW > kWaveTileFloats ? kWave * SG::OROW : kWaveTileFloats);
-  static_assert(kWave * D * 2 <= TILE, "scan must fit in the tile");
-  __shared__ __attribute__((aligned(16))) float tile[TILE];
-  __shared__ __attribute__((aligned(16))) float s_bank[SG::TT * 4];
-  __shared__ int64_t s_in[kWave], s_out[kWave];
-  __shared__ int s_len[kWave], s_lo[kWave];
-  double* scan = reinterpret_cast<double*>(tile);
-
-  const int c = threadIdx.x;  // chunk
-  const int64_t b = blockIdx.x;
-  // Tap bank: s_bank[v][p] = P[p][TT-1-v] = taps[p + L*(TT-1-v)] (0 past K).
-  for (int i = c; i < SG::TT * 4; i += kWave) {
-    const int v = i >> 2, ph = i & 3, k = ph + SG::L * (SG::TT - 1 - v);
-    s_bank[i] = (ph < SG::L && k < FS.K) ? FS.taps[k] : 0.f;
-  }
-  // Pass-1 rows: the x-domain state windows (k_iir_wave<P1 = 2>).
-  {
-    const int64_t start = (int64_t)c * XS.shift + XS.q0;
-    const bool need = c + 1 < C;
-    s_in[c] = need ? b * XS.ld + start : 0;
-    s_lo[c] = need ? (int)max((int64_t)0, -start) : 0;
-    s_len[c] = need ? (int)max((int64_t)0, min(XS.rows, XS.n - start)) : 0;
-    s_out[c] = 0;
-  }
-  const Rows rows{s_in, s_out, s_len, s_lo};
-  const __amdgpu_buffer_rsrc_t xin = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(XS.xs) + b * XS.ld, 0, (int)(XS.n * 4), 0x00020000);
-  const AffIO io1 = aff_rows(xin, XS.shift, XS.q0, 0, 0, c);
-
-  double s1[S], s2[S], e[D];
-#pragma unroll
-  for (int k = 0; k < S; ++k) s1[k] = s2[k] = 0.0;
-#pragma unroll
-  for (int i = 0; i < D; ++i) e[i] = 0.0;
-  const __amdgpu_buffer_rsrc_t zr =
-      __builtin_amdgcn_make_buffer_rsrc(z + b * ld, 0, (int)(n * 4), 0x00020000);
-
-  // ---- pass 1: zero-state end state of the lane's chunk, from x
-#if DSP_CHAIN_EXP != 6
-  run_pass<S, kStateTable, kWave, 1, true, true, true>(XS.xs, z, zr, tile, rows, io1, XS.rows, c,
-                                                       s1, s2, e, p, G, clip);
-#endif
-  // ---- carry scan
-  carry_scan<S, 1>(scan, e, s1, s2, sp, c, C);
-
-  // ---- pass 2: y = SRC(x) for the chunk, z = clip(cascade(y))
-  const AffIO io2 = aff_rows(xin, XS.shift, FS.nb0, 0, 0, c);
-  const __amdgpu_buffer_rsrc_t yr =
-      __builtin_amdgcn_make_buffer_rsrc(FS.y + b * ld, 0, (int)(n * 4), 0x00020000);
-  const float clo = clip ? -1.f : -INFINITY, chi = clip ? 1.f : INFINITY;
-  const int steps = PRO + (int)(T / NOUT);
-  const float* my = tile + c * kRow;
-  float* orow = tile + c * SG::OROW;
-  float win[WL];
-#pragma unroll
-  for (int i = 0; i < WL; ++i) win[i] = 0.f;
-  // Every path into the loop header has the next tile's loads followed by
-  // exactly 2*NOUT/4 stores (prologue tiles store out of range, the last
-  // tile's fetch reads out of range), so the compiler's wait for the loads is
-  // vmcnt(2*NOUT/4) and never drains the previous tile's y/z stores.
-  constexpr int kFar = 1 << 28;  // sample offset beyond any row: OOB, no traffic
-  float4 v[kLoads];
-  fetch_aff(v, io2, 0);
-  store_rows<SG>(yr, tile, T, kFar, c);
-  store_rows<SG>(zr, tile, T, kFar, c);
-  for (int kk = 0; kk < steps; ++kk) {
-    asm volatile("" ::: "memory");  // the previous tile's LDS reads come first
-    tile_put<kWave, false>(tile, v, rows, 0, c);
-    asm volatile("" ::: "memory");
-    fetch_aff(v, io2, kk + 1 < steps ? (kk + 1) * kTS : kFar);
-#pragma unroll
-    for (int i = 0; i < CR; ++i) win[i] = win[i + kTS];
-#pragma unroll
-    for (int j = 0; j < kTS; ++j) win[CR + j] = my[j];
-    if (kk < PRO) {
-      store_rows<SG>(yr, tile, T, kFar, c);
-      store_rows<SG>(zr, tile, T, kFar, c);
-      continue;
-    }
-#if DSP_CHAIN_EXP == 4
-    const int t0 = (kk - PRO) * 32;  // ablation: line-aligned partial stores
-#else
-    const int t0 = (kk - PRO) * NOUT;
-#endif
-    float acc[NOUT];
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i) acc[i] = 0.f;
-#if DSP_CHAIN_EXP == 1
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i) acc[i] = win[SG::q(i)] * 0.5f;
-#pragma unroll
-    for (int u = 0; u < 0; ++u) {
-#else
-#pragma unroll
-    for (int u = 0; u < SG::TT; ++u) {
-#endif
-      const float4 tq = *reinterpret_cast<const float4*>(s_bank + 4 * u);
-      const float tp[4] = {tq.x, tq.y, tq.z, tq.w};
-#pragma unroll
-      for (int i = 0; i < NOUT; ++i) acc[i] = fmaf(tp[SG::phi(i)], win[SG::q(i) + u], acc[i]);
-    }
-    asm volatile("" ::: "memory");  // x tile reads done before the y tile overwrites it
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i) orow[i] = acc[i];
-    asm volatile("" ::: "memory");
-#if DSP_CHAIN_EXP != 3
-    store_rows<SG>(yr, tile, T, t0, c);
-#endif
-    asm volatile("" ::: "memory");  // y reads done before z overwrites the tile
-#if DSP_CHAIN_EXP == 2
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i) orow[i] = clip_f32(acc[i] * 0.25f, clo, chi);
-#else
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i)
-      orow[i] = clip_f32((float)cascade_step<S, true>((double)acc[i], s1, s2, p), clo, chi);
-#endif
-    asm volatile("" ::: "memory");
-#if DSP_CHAIN_EXP != 3
-    store_rows<SG>(zr, tile, T, t0, c);
-#else
-    if (clip == 12345) store_rows<SG>(zr, tile, T, t0, c);
-#endif
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -897,19 +584,6 @@ __global__ __launch_bounds__(256) void k_iir_carry(const double* __restrict__ P,
   }
 }
 
-// One step of the realisation's state (w1_0, w2_0, w1_1, ...) with zero input:
-// the columns of A.  Host and device (general path) share it.
-__host__ __device__ inline void zero_input_step(const SosParams& p, int S, double* X) {
-  double u = 0.0;
-  for (int k = 0; k < S; ++k) {
-    const double w = u - p.c[k][3] * X[2 * k] - p.c[k][4] * X[2 * k + 1];
-    const double v = p.c[k][0] * w + p.c[k][1] * X[2 * k] + p.c[k][2] * X[2 * k + 1];
-    X[2 * k + 1] = X[2 * k];
-    X[2 * k] = w;
-    u = v;
-  }
-}
-
 // Builds A (one cascade step on each unit state, zero input) and P = A^T by
 // square-and-multiply in float64 inside one workgroup (general path; the fused
 // path gets A^T from the host as a kernel argument).
@@ -921,7 +595,7 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
   if (tid < D) {
     double X[32];
     for (int i = 0; i < D; ++i) X[i] = (i == tid) ? 1.0 : 0.0;
-    zero_input_step(p, S, X);
+    cascade_state_step(p, S, false, X, 0.0);
     for (int i = 0; i < D; ++i) sA[i * D + tid] = X[i];
   }
   const int r = tid / 32, c = tid % 32;
@@ -953,42 +627,6 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-// A of the D = 2S state system (state order w1_0, w2_0, w1_1, ...), float64.
-std::vector<double> state_matrix(const SosParams& p, int S) {
-  const int D = 2 * S;
-  std::vector<double> A((size_t)D * D, 0.0);
-  for (int col = 0; col < D; ++col) {
-    std::vector<double> X(D, 0.0);
-    X[col] = 1.0;
-    zero_input_step(p, S, X.data());
-    for (int r = 0; r < D; ++r) A[(size_t)r * D + col] = X[r];
-  }
-  return A;
-}
-
-std::vector<double> matmul(const std::vector<double>& a, const std::vector<double>& b, int D) {
-  std::vector<double> c((size_t)D * D, 0.0);
-  for (int i = 0; i < D; ++i)
-    for (int k = 0; k < D; ++k) {
-      const double aik = a[(size_t)i * D + k];
-      for (int j = 0; j < D; ++j)
-        c[(size_t)i * D + j] = std::fma(aik, b[(size_t)k * D + j], c[(size_t)i * D + j]);
-    }
-  return c;
-}
-
-// A^T by square-and-multiply.
-std::vector<double> chunk_transition(const SosParams& p, int S, int64_t T) {
-  const int D = 2 * S;
-  std::vector<double> base = state_matrix(p, S), r((size_t)D * D, 0.0);
-  for (int i = 0; i < D; ++i) r[(size_t)i * D + i] = 1.0;
-  for (int64_t e = T; e > 0; e >>= 1) {
-    if (e & 1) r = matmul(r, base, D);
-    if (e > 1) base = matmul(base, base, D);
-  }
-  return r;
-}
-
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct WsLayout {
@@ -1027,7 +665,7 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   const std::vector<double> P = chunk_transition(p, S, T);
   for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
   const int C = (int)ceil_div(n, T);
-  TraceScope trace(p1mode == 2 ? "iir_xstate" : p1mode == 3 ? "iir_ystate" : "iir_fused", s);
+  TraceScope trace(p1mode == 2 ? "iir_xstate" : "iir_fused", s);
   // VM: 1 = aligned rows of a length that is a multiple of 4, 2 = aligned rows
   // ending in a partial vector, 0 = any other pitch.  The buffer-store modes
   // address one channel's row with a 31-bit byte offset.
@@ -1054,10 +692,6 @@ int run_fused(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int6
   // The state tables are built for the NORM realisation (the EQ's); a cascade
   // with some b0 == 0 runs pass 1 as the cascade itself.
   if (!norm) { DSP_WAVE_VM(0, false) }
-  else if (p1mode == 3) {
-    if constexpr (2 * S == kStD) { DSP_WAVE_VM(3, true) }
-    else return set_error(DSP_EINVAL, "SRC-emitted chunk states need S = %d", kStD / 2);
-  }
   else if (p1mode == 2) { DSP_WAVE_VM(2, true) }
   else if (p1mode == 1) { DSP_WAVE_VM(1, true) }
   else { DSP_WAVE_VM(0, true) }
@@ -1194,100 +828,6 @@ int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t
                                     XS, s);
     default: return set_error(DSP_EINVAL, "unsupported stage count %d", S);
   }
-}
-
-namespace {
-bool x_aligned(const void* ptr, int64_t ld) {
-  return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(ptr) & 15) == 0;
-}
-
-template <int S, class SG>
-int run_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n, int64_t ld,
-                    const SosParams& p, int clip, int64_t T, const double* gx, const XState& XS,
-                    const float* taps, int K, int64_t a, hipStream_t s) {
-  ScanParams sp;
-  const std::vector<double> P = chunk_transition(p, S, T);
-  for (size_t i = 0; i < P.size(); ++i) sp.P[i] = P[i];
-  const int C = (int)ceil_div(n, T);
-  // Chunk 0's first new-sample block: window start a - (TT-1), plus the carry,
-  // minus the prologue blocks.
-  FusedSrc FS{y, taps, K, a - (SG::TT - 1) + SG::CR - (int64_t)kTS * SG::PRO};
-  TraceScope trace("chain_fused", s);
-  hipLaunchKernelGGL((k_chain_wave<S, SG>), dim3((unsigned)B), dim3(kWave), 0, s, z, n, ld, p,
-                     sp, gx, T, C, clip, XS, FS);
-  DSP_LAUNCHED("k_chain_wave");
-  return DSP_OK;
-}
-}  // namespace
-
-int launch_chain_fused(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
-                       int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
-                       int L, int M, int64_t c, const double* sos, int S, int clip,
-                       int64_t chunk_len, const double* gx, int64_t gx_rows, hipStream_t s) {
-  // Instantiated geometries: (L, M, ceil(K/L), c mod L) of the benchmark
-  // configurations 3/4 (3/2, K = 121) and the app's 2/1 with the default
-  // K = 81.  Anything else takes the two-launch chain.
-  const int TT = (K + L - 1) / L;
-  const int64_t a = c / L, bq = c % L;
-  int geo = 0;
-  if (L == 3 && M == 2 && TT == 41 && bq == 0) geo = 1;
-  if (L == 2 && M == 1 && TT == 41 && bq == 0) geo = 2;
-  if (!geo || S != 6 || !gx || !sos || !x_aligned(xs, ld_xs) || !x_aligned(y, ld_y) ||
-      !x_aligned(z, ld_y) || n_in % 4 || n_out % 4 || n_in * 4 + 16 >= (int64_t)kOob ||
-      n_out * 4 + 16 >= (int64_t)kOob || ld_xs < n_in || ld_y < n_out)
-    return kNotFused;
-  const int nout = geo == 1 ? SrcGeo<3, 2, 41, 0>::NOUT : SrcGeo<2, 1, 41, 0>::NOUT;
-  const int cr = geo == 1 ? SrcGeo<3, 2, 41, 0>::CR : SrcGeo<2, 1, 41, 0>::CR;
-  if (chunk_len % nout || (a - (TT - 1) + cr) % 4 != 0) return kNotFused;
-  const int64_t C = ceil_div(n_out, chunk_len);
-  if (!fused_ok(S, C, chunk_len) || C > kWave) return kNotFused;
-  SosParams p;
-  if (!realize(sos, S, &p)) return kNotFused;
-  XState XS{xs, ld_xs, n_in, 0, 0, 0};
-  if (int rc = xstate_geometry(chunk_len, K, L, M, c, &XS.shift, &XS.q0, &XS.rows)) return rc;
-  DSP_REQUIRE(gx_rows == XS.rows, "x-domain state table has %lld rows, geometry needs %lld",
-              (long long)gx_rows, (long long)XS.rows);
-  if (geo == 1)
-    return run_chain_fused<6, SrcGeo<3, 2, 41, 0>>(xs, y, z, B, n_out, ld_y, p, clip, chunk_len,
-                                                   gx, XS, taps, K, a, s);
-  return run_chain_fused<6, SrcGeo<2, 1, 41, 0>>(xs, y, z, B, n_out, ld_y, p, clip, chunk_len,
-                                                 gx, XS, taps, K, a, s);
-}
-
-size_t chain_states_bytes(int64_t B, int64_t n_out, int64_t chunk_len) {
-  if (B <= 0 || n_out <= 0 || chunk_len <= 0) return 0;
-  return (size_t)B * (size_t)ceil_div(n_out, chunk_len) * 2 * kStD * sizeof(double);
-}
-
-int launch_chain_ystate(const float* xs, float* y, float* z, int64_t B, int64_t n_in,
-                        int64_t ld_xs, int64_t n_out, int64_t ld_y, const float* taps, int K,
-                        int L, int M, int64_t c, const double* sos, int S, int clip,
-                        int64_t chunk_len, const double* state_table, void* ws,
-                        size_t ws_bytes, hipStream_t s) {
-  const int64_t tile = src_states_tile(L, M, K);
-  const int64_t C = chunk_len > 0 ? ceil_div(n_out, chunk_len) : 0;
-  if (!tile || 2 * S != kStD || !sos || !state_table || chunk_len <= 0 ||
-      chunk_len % kStU || chunk_len > tile || ceil_div(tile - 1, chunk_len) + 1 > kStPieces ||
-      !fused_ok(S, C, chunk_len) || ld_y < n_out || !ws ||
-      ws_bytes < chain_states_bytes(B, n_out, chunk_len) ||
-      (reinterpret_cast<uintptr_t>(ws) & 7))
-    return kNotFused;
-  SosParams p;
-  if (!realize(sos, S, &p)) return kNotFused;
-  SrcStates st;
-  st.part = static_cast<double*>(ws);
-  st.g = state_table + (chunk_len - kStU) * kStD;  // G[T - kStU + t] = A^(kStU-1-t) b
-  const std::vector<double> AU = chunk_transition(p, S, kStU);
-  for (int i = 0; i < kStD * kStD; ++i) st.AU[i] = AU[i];
-  st.chunk_len = chunk_len;
-  st.C = (int)C;
-  if (int rc = launch_src_states(xs, y, B, n_in, ld_xs, n_out, ld_y, taps, K, L, M, c, st, s))
-    return rc;
-  XState XS{};
-  XS.part = st.part;
-  XS.tile = tile;
-  return run_fused<6>(y, z, B, n_out, ld_y, ld_y, p, true, clip, chunk_len, state_table, 3,
-                      x_aligned(y, ld_y), x_aligned(z, ld_y), XS, s);
 }
 
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len) {

@@ -60,8 +60,10 @@ _SIGNATURES = {
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,
         _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
-    "dsp_chain_fusion": (ctypes.c_int, [_c_i32]),
-    "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i64]),
+    "dsp_chain_path": (ctypes.c_int, [_c_i32]),
+    "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
+    "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,
+                                          _c_i64, _c_i32, _c_i64]),
     "dsp_chain_xstate_geometry": (ctypes.c_int, [
         _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64),
         ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
@@ -132,14 +134,13 @@ def check(rc: int, what: str) -> None:
     raise RuntimeError(msg)
 
 
-def chain_fusion(mode: int = -1) -> int:
-    """Chain mode of dsp_chain_f32 on the calling thread (dsp_chain_fusion):
-    0 x-domain chunk states, 1 fused SRC + cascade launch, 2 chunk states
-    emitted by the SRC kernel (default); -1 only queries.  Returns the
-    previous mode."""
-    rc = load().dsp_chain_fusion(int(mode))
+def chain_path(path: int = -1) -> int:
+    """Path of dsp_chain_f32 on the calling thread (dsp_chain_path): 0 the
+    single-pass kernel where it applies (default), 1 always the two-launch
+    chain; -1 only queries.  Returns the previous setting."""
+    rc = load().dsp_chain_path(int(path))
     if rc < 0:
-        check(rc, "dsp_chain_fusion")
+        check(rc, "dsp_chain_path")
     return rc
 
 

@@ -3,6 +3,10 @@ app.py:203-205 for B channels at once, planned once and replayed.
 
 A Chain owns every device buffer (taps, LUTs, y, z, mag, workspace) so that
 `run()` is only kernel launches: graph-capturable, no allocation, no sync.
+
+Where the library has a single-pass kernel for the geometry
+(dsp_chain_tile_len > 0, include/dspcore.h) one launch computes y and z from x
+and a second the spectrum; otherwise SRC, cascade and spectrum run as three.
 """
 from __future__ import annotations
 
@@ -49,7 +53,10 @@ class Chain:
         spec_len = n_out if cfg.limit_pts is None else min(n_out, cfg.limit_pts)
         self.spec: SpectrumPlan = spectrum_plan(spec_len, cfg.n_fft)
         S = self.eq.sos.shape[0]
-        # x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
+        lib = _lib.load()
+        self.tile_len = 0 if self.identity_src else int(lib.dsp_chain_tile_len(
+            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S))
+        # Two-launch path (other geometries, or dsp_chain_path(1)): x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
         # the row into far fewer chunks than the plain rule.
         mc = max_chunks_for(self.B)
@@ -73,9 +80,11 @@ class Chain:
         self.z = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
         self.mag = torch.empty((self.B, self.spec.n_fft // 2 + 1), dtype=torch.float32,
                                device=dev)
-        ws_bytes = _lib.load().dsp_chain_workspace_bytes(self.B, n_out, self.sos.shape[0],
-                                                         self.chunk_len)
-        self.workspace = torch.empty(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
+        ws_bytes = lib.dsp_chain_workspace_bytes(self.B, cfg.n_in, n_out, self.src.K, self.src.L,
+                                                 self.src.M, self.src.c_offset, S, self.chunk_len)
+        # Zero-filled once: the single-pass kernel's hand-off flags start clear
+        # and every completed call leaves them clear (include/dspcore.h).
+        self.workspace = torch.zeros(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
         self.table = ops.state_table(self.sos, self.chunk_len, dev) if use_table else None
         self.xtable, self.xrows = (ops.xstate_table(self.sos, self.src, self.chunk_len, dev)
                                    if self.xstate else (None, 0))
@@ -85,6 +94,11 @@ class Chain:
         """4*N_in + 4*N_out (y) + 4*N_out (z) + 4*(N/2+1) per channel."""
         per = 4 * self.cfg.n_in + 8 * self.n_out + 4 * (self.spec.n_fft // 2 + 1)
         return per * self.B
+
+    def handoff_ok(self) -> bool:
+        """False if a single-pass call's tile hand-off wait gave up (workspace
+        word 0, include/dspcore.h); synchronises the device."""
+        return int(self.workspace[:4].view(torch.int32).item()) == 0
 
     def check_input(self, x: torch.Tensor) -> torch.Tensor:
         if x.shape != (self.B, self.cfg.n_in) or x.dtype != torch.float32 or not x.is_cuda:

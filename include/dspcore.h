@@ -146,12 +146,27 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   z   = clip(cascade(y))           (dsp_biquad_cascade_f32; S == 0 and
  *                                     clip == 0 is the EQ bypass: z := y)
  *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
- * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes().
- * Each row's result is bitwise independent of B.
+ * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes();
+ * the workspace must be zero-filled before its first use, and every completed
+ * call leaves it ready for the next one.  Each row's result is bitwise
+ * independent of B.
  *
- * Chunk end states of the cascade.  With `xstate_table` (device, float64
- * [xstate_rows][2S], may be NULL) the cascade's first pass reads x instead of
- * y: chunk c's zero-state end state is
+ * Single-pass path (default).  When dsp_chain_tile_len() is nonzero (today:
+ * (L, M, ceil(K/L)) = (3, 2, 41) with c_offset mod 3 == 0 and
+ * (c_offset/3 - 40) mod 4 == 0, S <= 6 with every b0 != 0, n_in and n_out
+ * multiples of 4) and the rows of x, y and z are 16-byte aligned with pitches
+ * that are multiples of 4, ONE kernel computes y and z from x: x is read once,
+ * y and z are written once, y is never read back.  Its y is bitwise that of
+ * dsp_src_polyphase_f32; z equals the two-launch chain's to float64 rounding.
+ * It derives its own state tables from sos_host (chunk_len, state_table and
+ * xstate_table are not used).  Workspace word 0 (uint32) is nonzero after a
+ * call whose tile hand-off wait gave up (a broken dispatch order; z is then
+ * wrong): a diagnostic, normally 0.
+ *
+ * Two-launch path (any other geometry, or dsp_chain_path(1)): SRC, then the
+ * cascade.  With `xstate_table` (device, float64 [xstate_rows][2S], may be
+ * NULL) the cascade's first pass reads x instead of y: chunk c's zero-state
+ * end state is
  *     E_c = sum_j xstate_table[j] * x[c*shift + q0 + j],   j < xstate_rows
  * (x == 0 outside [0, n_in)), where (shift, q0, xstate_rows) come from
  * dsp_chain_xstate_geometry and row j = sum_t G[t] (L h)[t*M + c_offset -
@@ -162,26 +177,15 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * Otherwise `state_table` (G, may be NULL) is used as in
  * dsp_biquad_cascade_f32.
  *
- * Chain modes, per calling thread (dsp_chain_fusion sets 0, 1 or 2 and returns
- * the previous mode, -1 only queries, anything else is DSP_EINVAL):
- *   0 (default)  SRC, then the cascade with the chunk states above;
- *   1  with the x-domain states, S == 6, n_in and n_out multiples of 4,
- *      16-byte aligned rows and an instantiated SRC geometry ((L, M, ceil(K/L),
- *      c_offset mod L) = (3, 2, 41, 0) or (2, 1, 41, 0)): ONE launch computes y
- *      from x in registers, stores it and filters it (y is never read back);
- *      y is bitwise the default SRC kernel's, z that of mode 0.  23 % fewer HBM
- *      bytes, measured slower;
- *   2  with `state_table` (G of chunk_len), S == 6, (L, M, ceil(K/L)) =
- *      (3, 2, 41), chunk_len a multiple of 96 in [288, 2880] and
- *      ceil(n_out / chunk_len) <= 256: the SRC kernel also emits every chunk's
- *      end state from the y tiles it holds (two float64 pieces per chunk in
- *      `workspace`) and the cascade skips its first pass; y is bitwise mode 0's,
- *      z equal to float64 rounding.  The cascade gets 30 % faster, the SRC
- *      twice as slow: measured slower.
- * A mode whose conditions do not hold runs as mode 0.
+ * dsp_chain_path sets the path for the calling thread: 0 (default) the
+ * single-pass kernel where it applies, 1 always the two-launch chain; -1 only
+ * queries; returns the previous setting (DSP_EINVAL for anything else).
  * ------------------------------------------------------------------------- */
-int dsp_chain_fusion(int32_t mode);
-size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_out, int32_t S,
+int dsp_chain_path(int32_t path);
+int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,
+                           int64_t c_offset, int32_t S);
+size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t K,
+                                 int32_t L, int32_t M, int64_t c_offset, int32_t S,
                                  int64_t chunk_len);
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
                               int64_t c_offset, int64_t* shift, int64_t* q0,

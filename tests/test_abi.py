@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 21
+    assert len(names) == 22
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -132,15 +132,24 @@ def test_wav_header_matches_scipy_writer():
     assert hdr.raw + pcm.tobytes() == buf.getvalue()
 
 
-def test_chain_mode_and_workspace_query():
-    """dsp_chain_fusion takes modes 0-2 (-1 queries); the chain workspace holds
-    the SRC-emitted chunk states (two float64 12-vectors per chunk)."""
+def test_chain_path_tile_len_and_workspace_query():
+    """dsp_chain_path takes 0/1 (-1 queries); dsp_chain_tile_len names the
+    single-pass geometry (config 3's L3/M2, K = 121: 48-sample sub-chunks) and
+    declines others; the chain workspace holds the tile hand-off (a 12-double
+    state and a flag per tile, 3072-output tiles) or the two-launch
+    cascade's scratch, whichever is larger."""
     lib = _lib.load()
-    prev = lib.dsp_chain_fusion(-1)
-    assert prev in (0, 1, 2)
-    assert lib.dsp_chain_fusion(3) == _lib.DSP_EINVAL
-    assert lib.dsp_chain_fusion(-1) == prev
-    B, n, T = 4096, 72000, 1152
-    C = -(-n // T)
-    assert lib.dsp_chain_workspace_bytes(B, n, 6, T) >= B * C * 2 * 12 * 8
-    assert lib.dsp_chain_workspace_bytes(B, n, 0, T) == 0
+    prev = lib.dsp_chain_path(-1)
+    assert prev in (0, 1)
+    assert lib.dsp_chain_path(2) == _lib.DSP_EINVAL
+    assert lib.dsp_chain_path(-1) == prev
+    assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 6) == 48
+    assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 3) == 48   # padded stages
+    assert lib.dsp_chain_tile_len(47996, 71994, 121, 3, 2, 60, 6) == 0    # n_out % 4
+    assert lib.dsp_chain_tile_len(48000, 52245, 1023, 160, 147, 511, 6) == 0
+    assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 7) == 0    # > 6 stages
+    B, n_in, n_out = 4096, 48000, 72000
+    tiles = -(-n_out // 3072)
+    ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)
+    assert ws >= B * tiles * (12 * 8 + 4)
+    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 1023, 160, 147, 511, 6, 1152) == 0

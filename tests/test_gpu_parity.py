@@ -33,14 +33,28 @@ def _dc():
 
 
 @contextlib.contextmanager
-def _chain_mode(mode):
-    """Chain mode of dsp_chain_f32 on this thread (dsp_chain_fusion)."""
+def _chain_path(path):
+    """Path of dsp_chain_f32 on this thread (dsp_chain_path): 0 single-pass
+    kernel where it applies, 1 always the two-launch chain."""
     from dspcore import _lib
-    prev = _lib.chain_fusion(mode)
+    prev = _lib.chain_path(path)
     try:
         yield
     finally:
-        _lib.chain_fusion(prev)
+        _lib.chain_path(prev)
+
+
+def _traced(fn):
+    """(results cloned, names of the kernels the library launched)."""
+    from dspcore import _lib
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    try:
+        out = tuple(t.clone() for t in fn())
+        names = [n for n, _ in _lib.trace_read()]
+    finally:
+        _lib.trace_enable(False)
+    return out, names
 
 
 def _ops():
@@ -313,17 +327,16 @@ def test_chain_matches_reference(gpu, tag, fs, L, M, K):
     ref = g[f"{tag}_mag"]
     assert np.max(np.abs(mag - ref)) <= CHAIN_MAG_RTOL * np.max(ref)
     # the staged path (one ABI call per stage): y bitwise; z within rounding of
-    # the fused chain, whose chunk states come from x through the composed
-    # table instead of from y (same float64 states up to ~1e-15 relative)
+    # the chain call, whose chunk states come from other chunkings (the
+    # single-pass kernel's 48-sample sub-chunks, or x-domain states)
     y2, z2, m2 = (t.cpu().numpy()[0] for t in ch.run_stages(x))
     np.testing.assert_array_equal(y2, y)
     assert np.max(np.abs(z2 - z)) <= 2e-6
     assert np.max(np.abs(m2 - mag)) <= 1e-5 * np.max(mag)
     if ch.xstate:
-        # and without x-domain (or SRC-emitted) states the chain call gives the
-        # staged bits
+        # and the two-launch chain without x-domain states gives the staged bits
         ch2 = Chain(cfg, 1, gpu, use_xstate=False, chunk_len=ch.chunk_len)
-        with _chain_mode(0):
+        with _chain_path(1):
             y3, z3, m3 = (t.cpu().numpy()[0] for t in ch2.run(x))
         np.testing.assert_array_equal(z3, z2)
         np.testing.assert_array_equal(m3, m2)
@@ -394,95 +407,68 @@ def test_shard_driver_bitwise_invariant(gpu):
             np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("L,M", [(3, 2), (2, 1)])
-def test_chain_fused_launch_matches_two_launch(gpu, L, M):
-    """The fused SRC + cascade launch (chain mode 1) against the two-launch
-    chain (mode 0) on the same plan: the fused kernel is the one that ran, y
-    agrees to float32 rounding (scalar fmaf chains vs the SRC kernel's packed
-    tap pairs), z and |X| within the EQ tolerance, rows match the reference."""
-    from dspcore import _lib
+@pytest.mark.parametrize("n_in,tile", [(48000, True), (4800, True), (96, True), (6144, True),
+                                       (47996, False), (100, False)])
+def test_chain_single_pass_matches_two_launch(gpu, n_in, tile):
+    """The single-pass chain kernel (csrc/chain_tile.hip) against the
+    two-launch chain on the same batch: it is the kernel that ran exactly where
+    dsp_chain_tile_len says so (n_out a multiple of 4: one tile, whole tiles,
+    a ragged last tile; otherwise the two-launch chain serves the call), y is
+    bitwise the SRC kernel's, z within float64 rounding of the two-launch z
+    (other chunking of the same recursion), |X| likewise; rows against the
+    reference recipe; the tile hand-off never gave up."""
     from dspcore.chain import Chain, ChainConfig
-    from dspcore.design import xstate_chunk_len
     from oracle import dsp_ref_cpu as orc
-    B, n_in = 6, 48000
-    cfg = ChainConfig(n_in, 48000, L, M, None, orc.CONFIG3_GAINS, n_fft=4096)
-    n_out = n_in * L // M
-    ch = Chain(cfg, B, gpu, chunk_len=xstate_chunk_len(n_out, L, M, 64))
-    assert ch.xstate and -(-n_out // ch.chunk_len) <= 64
+    B = 6
+    n_fft = 4096 if n_in >= 10000 else 2048 if n_in >= 2000 else 64
+    cfg = ChainConfig(n_in, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu)
+    assert (ch.tile_len > 0) == tile
     gen = torch.Generator(device=gpu).manual_seed(3)
     x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
     x[1] *= 40.0                      # drive the clip
     x[2, : n_in // 2] = 0.0           # silence then signal
-    runs = {}
-    prev = _lib.chain_fusion(-1)
-    try:
-        for mode in (1, 0):
-            _lib.chain_fusion(mode)
-            _lib.trace_enable(True)
-            _lib.trace_read()
-            y, z, mag = (t.clone() for t in ch.run(x))
-            names = [n for n, _ in _lib.trace_read()]
-            _lib.trace_enable(False)
-            runs[mode] = (y, z, mag, names)
-    finally:
-        _lib.chain_fusion(int(prev))
-    assert "chain_fused" in runs[1][3] and "src_poly" not in runs[1][3]
-    assert "chain_fused" not in runs[0][3]
-    (y1, z1, m1), (y0, z0, m0) = runs[1][:3], runs[0][:3]
-    assert (y1 - y0).abs().max().item() <= SRC_ATOL * max(1.0, y0.abs().max().item())
-    assert (z1 - z0).abs().max().item() <= EQ_ATOL
-    assert (m1 - m0).abs().max().item() <= CHAIN_MAG_RTOL * m0.abs().max().item()
-    y, z, mag = (t.cpu().numpy() for t in runs[1][:3])
-    assert np.abs(z[1]).max() == 1.0
-    for b in (0, 1, 2):
-        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, L, M, orc.CONFIG3_GAINS,
-                                       None, 4096)
-        assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
-        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
-        assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
-
-
-@pytest.mark.parametrize("n_in,chunk_len", [(48000, None), (48000, 1152), (47996, 1152)])
-def test_chain_src_emitted_states(gpu, n_in, chunk_len):
-    """Chain mode 2: the SRC kernel emits the cascade's chunk end states from
-    its y tiles (csrc/src_poly.hip emit_states) and the cascade skips its first
-    pass.  y bitwise that of mode 0, z within float64 rounding of it (the same
-    states summed in another order), rows against the reference recipe; both
-    batch regimes' chunkings (288 / 1152 samples) and a row whose length is
-    not a multiple of 4 (unaligned pitch, partial last tile and chunk)."""
-    from dspcore import _lib
-    from dspcore.chain import Chain, ChainConfig
-    from oracle import dsp_ref_cpu as orc
-    B = 6
-    cfg = ChainConfig(n_in, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=4096)
-    ch = Chain(cfg, B, gpu, chunk_len=chunk_len)
-    gen = torch.Generator(device=gpu).manual_seed(11)
-    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
-    x[1] *= 40.0                      # drive the clip
-    x[2, : n_in // 2] = 0.0           # silence then signal
-    runs = {}
-    for mode in (2, 0):
-        with _chain_mode(mode):
-            _lib.trace_enable(True)
-            _lib.trace_read()
-            y, z, mag = (t.clone() for t in ch.run(x))
-            names = [n for n, _ in _lib.trace_read()]
-            _lib.trace_enable(False)
-        runs[mode] = (y, z, mag, names)
-    assert "src_states" in runs[2][3] and "iir_ystate" in runs[2][3], runs[2][3]
-    assert "src_states" not in runs[0][3]
-    assert torch.equal(runs[2][0], runs[0][0])
-    assert (runs[2][1] - runs[0][1]).abs().max().item() <= 2e-6
-    m2, m0 = runs[2][2], runs[0][2]
-    assert (m2 - m0).abs().max().item() <= 1e-5 * m0.abs().max().item()
-    y, z, mag = (t.cpu().numpy() for t in runs[2][:3])
+    (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
+    with _chain_path(1):
+        (y0, z0, m0), names0 = _traced(lambda: ch.run(x))
+    assert ("chain_tile" in names1 and "src_poly" not in names1) == tile, names1
+    assert "chain_tile" not in names0 and "src_poly" in names0, names0
+    assert ch.handoff_ok()
+    assert torch.equal(y1, y0)
+    assert (z1 - z0).abs().max().item() <= 2e-6
+    assert (m1 - m0).abs().max().item() <= 1e-5 * m0.abs().max().item()
+    y, z, mag = (t.cpu().numpy() for t in (y1, z1, m1))
     assert np.abs(z[1]).max() == 1.0
     for b in (0, 1, 2, 5):
         ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, orc.CONFIG3_GAINS,
-                                       None, 4096)
+                                       None, cfg.n_fft)
         assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
         assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
         assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+
+
+@pytest.mark.parametrize("gains", [{"Sub-Bass": 6, "Bass": 0.0, "Presence": -3, "Otra": 4},
+                                   {"Sub-Bass": 0, "Bass": 0.05}])
+def test_chain_single_pass_fewer_bands_and_bypass(gpu, gains):
+    """Fewer than six bands run through the single-pass kernel padded with
+    exact identity stages; an all-bypass EQ (sistema_ecualizador returns its
+    input, dsp_core.py:222-223) gives z == y bitwise with no clip."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    cfg = ChainConfig(48000, 48000, 3, 2, None, gains, n_fft=4096)
+    ch = Chain(cfg, 3, gpu)
+    assert ch.tile_len > 0
+    gen = torch.Generator(device=gpu).manual_seed(5)
+    x = (torch.rand((3, 48000), generator=gen, device=gpu) * 2 - 1) * 3.0
+    (y, z, mag), names = _traced(lambda: ch.run(x))
+    assert "chain_tile" in names
+    if ch.eq.bypass:
+        assert torch.equal(y, z) and z.abs().max().item() > 1.0
+    for b in range(3):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, gains, None, 4096)
+        assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL * max(1.0, np.abs(rz).max())
+        assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
 
 
 def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
@@ -497,8 +483,8 @@ def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
     ch = Chain(cfg, 3, gpu)
     gen = torch.Generator(device=gpu).manual_seed(13)
     x = torch.rand((3, n_in), generator=gen, device=gpu) * 2 - 1
-    with _chain_mode(0):
-        y, z, mag = (t.clone() for t in ch.run(x))
+    assert ch.tile_len == 0           # n_in % 4 != 0: the two-launch chain
+    y, z, mag = (t.clone() for t in ch.run(x))
     y2, z2, m2 = ch.run_stages(x)
     assert torch.equal(y, y2) and torch.equal(z, z2) and torch.equal(mag, m2)
     for b in range(3):
