@@ -19,15 +19,30 @@
 //      window, read from the tile's x window in LDS (one coalesced load per
 //      tile, padded so the 64 lanes' ds_read_b128 are conflict-free).  Same
 //      per-output FMA order as k_src_reg: y is bitwise the SRC kernel's.
-//   2. pass 1: the sub-chunk's zero-state end state E_l: the cascade run over
-//      the lane's TSUB outputs from zero state (float64).
-//   3. carry: the tile's entry state S_in comes from the previous tile of the
-//      same channel (chained hand-off, below); 12 lanes run the serial scan
-//      S_{l+1} = A^TSUB S_l + E_l over the 64 sub-chunks in LDS, float64.
-//   4. the tile's end state S_64 is published for the next tile;
-//   5. y leaves through LDS as coalesced float4 stores; pass 2 reruns the
-//      cascade over the lane's sub-chunk from S_l, clips, and z leaves the
-//      same way.
+//   2. pass 1: the sub-chunk's zero-state end state, in block-diagonal
+//      coordinates (below): E'_l = sum_i G'[i] y[i], G'[i] = T^-1 A^(TSUB-1-i) B
+//      (wave-uniform, float64), 12 FMAs per sample;
+//   3. carry: the tile's entry state m_in comes from the previous tile of the
+//      same channel (chained hand-off, below); an inclusive Kogge-Stone scan
+//      across the 64 lanes, v_l += D^(TSUB 2^d) v_(l-2^d) for d = 0..5, gives
+//      every sub-chunk's entry state m_l = v_(l-1) (m_0 = m_in, folded into
+//      lane 0 as v_0 = D^TSUB m_in + E'_0);
+//   4. lane 63's v (the tile's end state) is published for the next tile;
+//   5. y leaves through LDS as coalesced float4 stores; the lane's DF2 state
+//      is s_l = T m_l and pass 2 reruns the cascade over the sub-chunk from it,
+//      clips, and z leaves the same way.
+//
+// Block-diagonal coordinates.  The cascade's state matrix A is block lower
+// triangular (stage k is driven by stage k-1's output) with 2x2 diagonal
+// blocks A_kk.  With T block unit lower triangular solving A T = T D,
+// D = diag(A_kk) (Sylvester equations A_ii X - X A_jj = C for the off-diagonal
+// blocks, solvable when no two stages share a pole pair), A^N = T D^N T^-1 and
+// powers of D are six independent 2x2 powers: the carry costs 4 FMAs per block
+// per scan level instead of a dense 12x12 product.  Stages that only pad the
+// cascade to six (exact identities) have states no output depends on; their
+// coordinates are dropped.  The host computes T, D's powers and checks the
+// conditioning in float64; a cascade without a well-conditioned T takes the
+// two-launch chain.
 // y never returns from HBM, and there is no second pass over x.
 //
 // Chained hand-off.  Workgroups are numbered tile-major (id = tile*B + b), so
@@ -45,6 +60,8 @@
 //
 // Rows are bitwise independent of the batch size: the geometry depends on
 // (L, M, K) only.
+#include <algorithm>
+
 #include "cascade.h"
 
 namespace dsp {
@@ -82,23 +99,35 @@ struct TileGeo {
   static_assert(L <= 4, "one float4 of taps per tap index");
 };
 
+// Block-diagonal carry tables, float64, in the workspace (k_tile_prep).
+struct ModalTables {
+  double G[64][kD];        // G'[i], i < TSUB
+  double Dp[6][kS][4];     // D_k^(TSUB 2^d), row-major 2x2, d = 0..5
+  double T[kD][kD];        // s = T m (row-major; zero rows/cols: padding stages)
+};
+
+// Kernel argument of k_tile_prep: B' = T^-1 B and the diagonal blocks, from
+// which it builds G'; the powers and T are copied as they are.
+struct ModalSeed {
+  double Bp[kD];
+  double Dk[kS][4];
+  double Dp[6][kS][4];
+  double T[kD][kD];
+  int tsub;
+};
+
 struct TileArgs {
   const float* x;
   float* y;
   float* z;
-  const float* taps;  // float32 L*h[K]
-  const double* P;    // A^TSUB [12][12] in the workspace (k_tile_prep)
-  double* states;     // [B][ntiles][12] tile end states
-  uint32_t* flags;    // [B][ntiles]
-  uint32_t* err;      // set when a hand-off wait gave up
+  const float* taps;        // float32 L*h[K]
+  const ModalTables* mt;    // in the workspace
+  double* states;           // [B][ntiles][12] tile end states (block-diagonal coords)
+  uint32_t* flags;          // [B][ntiles]
+  uint32_t* err;            // set when a hand-off wait gave up
   int64_t B, n_in, ld_x, n_out, ld_y, ntiles, cq;
   int K, clip;
   SosParams p;
-};
-
-// Host -> workspace copy of A^TSUB (kernel argument of k_tile_prep).
-struct PMat {
-  double v[kD * kD];
 };
 
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
@@ -110,6 +139,22 @@ template <int N, class T>
 __device__ __forceinline__ void pin(T (&v)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+// 2x2 block of v <- M v + acc (M row-major; any address space).
+template <class PTR>
+__device__ __forceinline__ void mac2(PTR M, double x0, double x1, double& a0, double& a1) {
+  a0 = fma(M[0], x0, fma(M[1], x1, a0));
+  a1 = fma(M[2], x0, fma(M[3], x1, a1));
+}
+
+__device__ __forceinline__ double shfl_up_f64(double v, int d) {
+  // ds_bpermute (the LDS crossbar, no LDS memory): lane l reads lane l - d.
+  const int src = ((int)threadIdx.x - d) << 2;
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 // Agent-scope hand-off accesses: global (never flat) loads/stores with sc1.
@@ -214,6 +259,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   const int64_t id = blockIdx.x;
   const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
   const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
+  typedef __attribute__((address_space(4))) const ModalTables* mt_ptr;
+  const mt_ptr mt = (mt_ptr)a.mt;  // wave-uniform: scalar loads
 
   // ---- tap bank: bank[u][ph] = taps[ph + L*(TT-1-u)] (0 past K): tap u of
   // branch ph in the reversed order the SRC sums in.
@@ -250,102 +297,134 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     pin(y);
   }
 
-  // ---- 2. pass 1: zero-state end state of the sub-chunk
-  double e[kD];
-  {
-    double w1[kS], w2[kS];
+  // ---- 2. pass 1: zero-state end state of the sub-chunk, block-diagonal coords
+  double v[kD];
 #pragma unroll
-    for (int k = 0; k < kS; ++k) w1[k] = w2[k] = 0.0;
+  for (int d = 0; d < kD; ++d) v[d] = 0.0;
 #pragma unroll
-    for (int i = 0; i < TS; ++i) (void)cascade_step<kS, true>((double)y[i], w1, w2, a.p);
+  for (int i = 0; i < TS; ++i) {
+    const double u = (double)y[i];
 #pragma unroll
-    for (int k = 0; k < kS; ++k) {
-      e[2 * k] = w1[k];
-      e[2 * k + 1] = w2[k];
-    }
+    for (int d = 0; d < kD; ++d) v[d] = fma(mt->G[i][d], u, v[d]);
   }
   // Keep the SRC and pass 1 ahead of the hand-off wait (the compiler would
   // otherwise sink them past it).
-  pin(e);
+  pin(v);
 
-  // ---- 3. entry state of the tile, then the carry scan over the sub-chunks
-  double s_in = 0.0;
-  if (tile > 0) {
+  // ---- 3. entry state of the tile (lane 0), then the scan across the lanes
+  double m_in[kD];
+#pragma unroll
+  for (int d = 0; d < kD; ++d) m_in[d] = 0.0;
+  if (tile > 0 && lane == 0) {
     const int64_t prev = b * a.ntiles + tile - 1;
-    if (lane == 0) {
-      uint32_t spins = 0;
-      while (load_flag(a.flags + prev) == 0u) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins == kMaxSpins) {
-          store_flag(a.err, 1u);
-          break;
-        }
+    uint32_t spins = 0;
+    while (load_flag(a.flags + prev) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins == kMaxSpins) {
+        store_flag(a.err, 1u);
+        break;
       }
     }
     fence();
-    if (lane < kD) s_in = load_state(a.states + prev * kD + lane);
-    if (lane == 0) store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
+#pragma unroll
+    for (int d = 0; d < kD; ++d) m_in[d] = load_state(a.states + prev * kD + d);
+    store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
+    // v_0 = D^TSUB m_in + E'_0
+#pragma unroll
+    for (int k = 0; k < kS; ++k)
+      mac2(mt->Dp[0][k], m_in[2 * k], m_in[2 * k + 1], v[2 * k], v[2 * k + 1]);
   }
-  fence();
-  double* sc = reinterpret_cast<double*>(lds);  // slot j = S_j (j = 0..64)
 #pragma unroll
-  for (int d = 0; d < kD; ++d) sc[(1 + lane) * kD + d] = e[d];
-  if (lane < kD) sc[lane] = s_in;
-  fence();
-  if (lane < kD) {
-    double prow[kD];
+  for (int lv = 0; lv < 6; ++lv) {
+    const int off = 1 << lv;
+    double x[kD];
 #pragma unroll
-    for (int j = 0; j < kD; ++j) prow[j] = a.P[lane * kD + j];  // lane-varying: vector loads
-    for (int cc = 0; cc < kWave; ++cc) {
-      const double* s = sc + cc * kD;
-      double a0 = sc[(1 + cc) * kD + lane], a1 = 0.0, a2 = 0.0;
+    for (int d = 0; d < kD; ++d) x[d] = shfl_up_f64(v[d], off);
+    if (lane >= off) {
 #pragma unroll
-      for (int j = 0; j < kD; j += 3) {
-        a0 = fma(prow[j], s[j], a0);
-        a1 = fma(prow[j + 1], s[j + 1], a1);
-        a2 = fma(prow[j + 2], s[j + 2], a2);
-      }
-      fence();  // every lane's reads of S_cc precede the write
-      sc[(1 + cc) * kD + lane] = (a0 + a1) + a2;
-      fence();
+      for (int k = 0; k < kS; ++k) mac2(mt->Dp[lv][k], x[2 * k], x[2 * k + 1], v[2 * k], v[2 * k + 1]);
     }
   }
-  fence();
-
-  // ---- 4. publish the tile's end state for the next tile of the channel
-  if (tile + 1 < a.ntiles) {
-    const int64_t me = b * a.ntiles + tile;
-    if (lane < kD) store_state(a.states + me * kD + lane, sc[kWave * kD + lane]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) store_flag(a.flags + me, 1u);
-  }
-
-  double s1[kS], s2[kS];
+  // Entry state of the lane's sub-chunk: v of the lane before (m_in for lane 0).
+  double m[kD];
 #pragma unroll
-  for (int k = 0; k < kS; ++k) {
-    s1[k] = sc[lane * kD + 2 * k];
-    s2[k] = sc[lane * kD + 2 * k + 1];
+  for (int d = 0; d < kD; ++d) {
+    const double t = shfl_up_f64(v[d], 1);
+    m[d] = lane == 0 ? m_in[d] : t;
   }
-  fence();
 
-  // ---- 5. y out, pass 2, z out
+  // ---- 4. publish the tile's end state (lane 63) for the next tile
+  if (tile + 1 < a.ntiles && lane == kWave - 1) {
+    const int64_t me = b * a.ntiles + tile;
+#pragma unroll
+    for (int d = 0; d < kD; ++d) store_state(a.states + me * kD + d, v[d]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_flag(a.flags + me, 1u);
+  }
+
+  // ---- 5. y out, DF2 entry state s = T m, pass 2, z out
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   store_tile<GEO>(lds, y, lane, ry, m0);
   pin(y);
-  const float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+  double s1[kS], s2[kS];
 #pragma unroll
-  for (int i = 0; i < TS; ++i)
-    y[i] = clip_f32((float)cascade_step<kS, true>((double)y[i], s1, s2, a.p), lo, hi);
+  for (int r = 0; r < kD; ++r) {
+    double acc = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < (r / 2 + 1) * 2; ++cc) acc = fma(mt->T[r][cc], m[cc], acc);
+    if (r & 1) s2[r / 2] = acc;
+    else s1[r / 2] = acc;
+  }
+  // Pass 2, diagonally pipelined: step s runs stage k on sample s - k, so the
+  // six stage updates of a step are independent (six FMA chains in flight
+  // instead of one 24-deep chain per sample).  Per sample and stage the
+  // operations are cascade_step's: the results are bitwise the same.
+  const float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+  {
+    double pend[kS];  // pend[k]: stage k's output from the previous step
+#pragma unroll
+    for (int st = 0; st < TS + kS - 1; ++st) {
+#pragma unroll
+      for (int k = kS - 1; k >= 0; --k) {
+        const int t = st - k;
+        if (t < 0 || t >= TS) continue;
+        const double u = k == 0 ? (double)y[t] * a.p.G : pend[k - 1];
+        const double* cf = a.p.c[k];
+        const double w = fma(-cf[4], s2[k], fma(-cf[3], s1[k], u));
+        const double v = fma(cf[2], s2[k], fma(cf[1], s1[k], w));
+        s2[k] = s1[k];
+        s1[k] = w;
+        if (k == kS - 1) y[t] = clip_f32((float)v, lo, hi);
+        else pend[k] = v;
+      }
+    }
+  }
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-  store_tile<GEO>(lds, y, lane, rz, m0);
+  int lane_z = lane;
+  asm volatile("" : "+v"(lane_z));  // recompute the store offsets (no spill across pass 2)
+  store_tile<GEO>(lds, y, lane_z, rz, m0);
 }
 
-// A^TSUB (computed on the host in float64) into the workspace, where the scan
-// lanes read their rows with vector loads.
-__global__ __launch_bounds__(kWave) void k_tile_prep(PMat m, double* P) {
-  for (int i = threadIdx.x; i < kD * kD; i += kWave) P[i] = m.v[i];
+// Block-diagonal tables into the workspace: lane i < tsub builds
+// G'[i] = D^(tsub-1-i) B' (2x2 block powers), the rest is copied.
+__global__ __launch_bounds__(kWave) void k_tile_prep(ModalSeed sd, ModalTables* mt) {
+  const int i = threadIdx.x;
+  if (i < sd.tsub) {
+    double g[kD];
+    for (int d = 0; d < kD; ++d) g[d] = sd.Bp[d];
+    for (int s = 0; s < sd.tsub - 1 - i; ++s)
+      for (int k = 0; k < kS; ++k) {
+        const double* M = sd.Dk[k];
+        const double g0 = g[2 * k], g1 = g[2 * k + 1];
+        g[2 * k] = M[0] * g0 + M[1] * g1;
+        g[2 * k + 1] = M[2] * g0 + M[3] * g1;
+      }
+    for (int d = 0; d < kD; ++d) mt->G[i][d] = g[d];
+  }
+  for (int j = i; j < 6 * kS * 4; j += kWave) (&mt->Dp[0][0][0])[j] = (&sd.Dp[0][0][0])[j];
+  for (int j = i; j < kD * kD; j += kWave) (&mt->T[0][0])[j] = (&sd.T[0][0])[j];
 }
 
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
@@ -373,6 +452,128 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Solves the 4x4 system M z = r in place (partial pivoting); false if singular
+// to working precision.
+bool solve4(double M[4][4], double r[4]) {
+  for (int c = 0; c < 4; ++c) {
+    int piv = c;
+    for (int i = c + 1; i < 4; ++i)
+      if (std::fabs(M[i][c]) > std::fabs(M[piv][c])) piv = i;
+    if (!(std::fabs(M[piv][c]) > 1e-13)) return false;
+    if (piv != c) {
+      for (int j = 0; j < 4; ++j) std::swap(M[c][j], M[piv][j]);
+      std::swap(r[c], r[piv]);
+    }
+    for (int i = c + 1; i < 4; ++i) {
+      const double f = M[i][c] / M[c][c];
+      for (int j = c; j < 4; ++j) M[i][j] -= f * M[c][j];
+      r[i] -= f * r[c];
+    }
+  }
+  for (int c = 3; c >= 0; --c) {
+    double s = r[c];
+    for (int j = c + 1; j < 4; ++j) s -= M[c][j] * r[j];
+    r[c] = s / M[c][c];
+  }
+  return true;
+}
+
+// Block-diagonal form of the first 2*Sr states (the real stages): T block
+// unit lower triangular with A T = T D, D = diag(A_kk).  Fills the kernel's
+// seed (G' generator B' = T^-1 B, D blocks and their powers, T); false when
+// two stages share a pole pair or T is ill-conditioned.
+bool modal_seed(const SosParams& p, int Sr, int tsub, ModalSeed* sd) {
+  const int n = 2 * Sr;
+  const std::vector<double> A = state_matrix(p, kS);  // 12 x 12
+  auto Aat = [&](int r, int c) { return A[(size_t)r * kD + c]; };
+  std::vector<double> T((size_t)kD * kD, 0.0);
+  for (int i = 0; i < n; ++i) T[(size_t)i * kD + i] = 1.0;
+  for (int j = 0; j < Sr; ++j) {
+    for (int i = j + 1; i < Sr; ++i) {
+      // A_ii X - X A_jj = -sum_{l=j}^{i-1} A_il T_lj
+      double C[2][2] = {{0, 0}, {0, 0}};
+      for (int l = j; l < i; ++l)
+        for (int r = 0; r < 2; ++r)
+          for (int c = 0; c < 2; ++c)
+            for (int q = 0; q < 2; ++q)
+              C[r][c] -= Aat(2 * i + r, 2 * l + q) * T[(size_t)(2 * l + q) * kD + 2 * j + c];
+      // vec (column-major): (I (x) A_ii - A_jj^T (x) I) vec(X) = vec(C)
+      double M[4][4], rhs[4];
+      for (int cc = 0; cc < 2; ++cc)
+        for (int rr = 0; rr < 2; ++rr) {
+          const int row = cc * 2 + rr;
+          rhs[row] = C[rr][cc];
+          for (int c2 = 0; c2 < 2; ++c2)
+            for (int r2 = 0; r2 < 2; ++r2) {
+              const int col = c2 * 2 + r2;
+              double v = 0.0;
+              if (c2 == cc) v += Aat(2 * i + rr, 2 * i + r2);
+              if (r2 == rr) v -= Aat(2 * j + c2, 2 * j + cc);
+              M[row][col] = v;
+            }
+        }
+      if (!solve4(M, rhs)) return false;
+      for (int cc = 0; cc < 2; ++cc)
+        for (int rr = 0; rr < 2; ++rr) T[(size_t)(2 * i + rr) * kD + 2 * j + cc] = rhs[cc * 2 + rr];
+    }
+  }
+  // T^-1 (unit lower triangular: forward substitution per column).
+  std::vector<double> Ti((size_t)kD * kD, 0.0);
+  for (int c = 0; c < n; ++c)
+    for (int r = 0; r < n; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+      for (int q = 0; q < r; ++q) s -= T[(size_t)r * kD + q] * Ti[(size_t)q * kD + c];
+      Ti[(size_t)r * kD + c] = s;
+    }
+  double nT = 0.0, nTi = 0.0;
+  for (int r = 0; r < n; ++r) {
+    double a = 0.0, b2 = 0.0;
+    for (int c = 0; c < n; ++c) {
+      a += std::fabs(T[(size_t)r * kD + c]);
+      b2 += std::fabs(Ti[(size_t)r * kD + c]);
+    }
+    nT = std::max(nT, a);
+    nTi = std::max(nTi, b2);
+  }
+  if (!(nT * nTi < 1e8)) return false;
+  // B of the realisation (includes the input gain), then B' = T^-1 B.
+  double Bv[kD] = {0};
+  cascade_state_step(p, kS, true, Bv, 1.0);
+  for (int r = 0; r < kD; ++r) {
+    double s = 0.0;
+    for (int c = 0; c < n; ++c) s += Ti[(size_t)r * kD + c] * Bv[c];
+    sd->Bp[r] = r < n ? s : 0.0;
+  }
+  for (int k = 0; k < kS; ++k) {
+    double Dk[4] = {0, 0, 0, 0};
+    if (k < Sr)
+      for (int q = 0; q < 4; ++q) Dk[q] = Aat(2 * k + q / 2, 2 * k + q % 2);
+    for (int q = 0; q < 4; ++q) sd->Dk[k][q] = Dk[q];
+    // D_k^tsub by square-and-multiply, then repeated squaring per level.
+    double R[4] = {1, 0, 0, 1}, Bq[4] = {Dk[0], Dk[1], Dk[2], Dk[3]};
+    auto mul = [](const double* X, const double* Y, double* Z) {
+      const double z0 = X[0] * Y[0] + X[1] * Y[2], z1 = X[0] * Y[1] + X[1] * Y[3];
+      const double z2 = X[2] * Y[0] + X[3] * Y[2], z3 = X[2] * Y[1] + X[3] * Y[3];
+      Z[0] = z0;
+      Z[1] = z1;
+      Z[2] = z2;
+      Z[3] = z3;
+    };
+    for (int e = tsub; e > 0; e >>= 1) {
+      if (e & 1) mul(R, Bq, R);
+      if (e > 1) mul(Bq, Bq, Bq);
+    }
+    for (int d = 0; d < 6; ++d) {
+      for (int q = 0; q < 4; ++q) sd->Dp[d][k][q] = k < Sr ? R[q] : 0.0;
+      mul(R, R, R);
+    }
+  }
+  for (int r = 0; r < kD; ++r)
+    for (int c = 0; c < kD; ++c) sd->T[r][c] = (r < n && c < n) ? T[(size_t)r * kD + c] : 0.0;
+  sd->tsub = tsub;
+  return true;
+}
+
 struct TileWs {
   size_t err_off, g_off, st_off, fl_off, total;
 };
@@ -380,8 +581,8 @@ struct TileWs {
 TileWs tile_ws(int64_t B, int64_t ntiles, int64_t tsub) {
   TileWs w;
   w.err_off = 0;  // include/dspcore.h: the workspace's first word
-  w.g_off = 256;  // A^TSUB
-  w.st_off = w.g_off + align256((size_t)kD * kD * sizeof(double));
+  w.g_off = 256;  // ModalTables
+  w.st_off = w.g_off + align256(sizeof(ModalTables));
   w.fl_off = w.st_off + align256((size_t)B * ntiles * kD * sizeof(double));
   w.total = w.fl_off + align256((size_t)B * ntiles * sizeof(uint32_t));
   return w;
@@ -414,6 +615,8 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   SosParams p;
   if (S > 0 && !realize(sos, S, &p)) return kNotFused;  // a b0 == 0 band: no NORM form
   if (S == 0) realize(nullptr, 0, &p);
+  ModalSeed sd;
+  if (!modal_seed(p, S, (int)tp.tsub, &sd)) return kNotFused;  // shared poles: two-launch
   const TileWs w = tile_ws(B, tp.ntiles, tp.tsub);
   DSP_REQUIRE(ws && ws_bytes >= w.total, "chain workspace too small: %zu < %zu bytes", ws_bytes,
               w.total);
@@ -425,7 +628,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.y = y;
   a.z = z;
   a.taps = taps;
-  a.P = reinterpret_cast<const double*>(base + w.g_off);
+  a.mt = reinterpret_cast<const ModalTables*>(base + w.g_off);
   a.states = reinterpret_cast<double*>(base + w.st_off);
   a.flags = reinterpret_cast<uint32_t*>(base + w.fl_off);
   a.err = reinterpret_cast<uint32_t*>(base + w.err_off);
@@ -439,13 +642,10 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.K = K;
   a.clip = clip;
   a.p = p;
-  PMat pm;
-  const std::vector<double> P = chunk_transition(p, kS, tp.tsub);
-  for (int i = 0; i < kD * kD; ++i) pm.v[i] = P[i];
   {
     TraceScope trace("chain_prep", s);
-    hipLaunchKernelGGL(k_tile_prep, dim3(1), dim3(kWave), 0, s, pm,
-                       reinterpret_cast<double*>(base + w.g_off));
+    hipLaunchKernelGGL(k_tile_prep, dim3(1), dim3(kWave), 0, s, sd,
+                       reinterpret_cast<ModalTables*>(base + w.g_off));
   }
   DSP_LAUNCHED("k_tile_prep");
   {

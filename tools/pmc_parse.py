@@ -14,15 +14,17 @@ from collections import defaultdict
 
 def short(name):
     """Bench-trace name of a libdspcore kernel from its demangled symbol."""
-    if "k_src_reg" in name and ", true>" in name:
-        return "src_states"
+    if "k_chain_tile" in name:
+        return "chain_tile"
+    if "k_tile_prep" in name:
+        return "chain_prep"
     if "k_src" in name:
         return "src_poly"
-    if "k_chain_wave" in name:
-        return "chain_fused"
+    if "k_spec_real" in name:
+        return "spectrum"
     m = re.search(r"k_iir_wave<(\d+), (\d+)", name)
     if m:
-        return {"2": "iir_xstate", "3": "iir_ystate"}.get(m.group(2), "iir_fused")
+        return {"2": "iir_xstate"}.get(m.group(2), "iir_fused")
     m = re.search(r"k_iir_pass<(\d+), (true|false)", name)
     if m:
         return "iir_apply" if m.group(2) == "true" else "iir_state"
