@@ -151,6 +151,16 @@ size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t
   return a > b ? a : b;
 }
 
+size_t dsp_chain_tile_tables_bytes(void) { return dsp::chain_tile_tables_bytes(); }
+
+int dsp_chain_tile_tables(void* tables_host, size_t tables_bytes, int64_t n_in, int64_t n_out,
+                          const float* taps_host, int32_t K, int32_t L, int32_t M,
+                          int64_t c_offset, const double* sos_host, int32_t S) {
+  dsp::clear_error();
+  return dsp::chain_tile_tables(tables_host, tables_bytes, n_in, n_out, taps_host, K, L, M,
+                                c_offset, sos_host, S);
+}
+
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
                               int64_t c_offset, int64_t* shift, int64_t* q0, int64_t* rows) {
   dsp::clear_error();
@@ -162,7 +172,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                   int64_t ld_x, int64_t n_out, int64_t ld_y, const float* taps, int32_t K,
                   int32_t L, int32_t M, int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
-                  const double* xstate_table, int64_t xstate_rows, int64_t seg_start,
+                  const double* xstate_table, int64_t xstate_rows, const void* tile_tables,
+                  int64_t seg_start,
                   int64_t seg_len, int32_t log2n, int64_t ld_mag, const float* window,
                   const float* twiddles, void* workspace, size_t workspace_bytes,
                   void* stream) {
@@ -172,8 +183,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   if (B == 0) return DSP_OK;
   int rc = dsp::kNotFused;
   if (dsp::g_chain_path == 0)
-    rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
-                                sos_host, S, clip, workspace, workspace_bytes, s);
+    rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, K, L, M, c_offset, sos_host,
+                                S, clip, tile_tables, workspace, workspace_bytes, s);
   if (rc == dsp::kNotFused) {
     // Two-launch chain: SRC, then the cascade with x-domain chunk states where
     // the input rows are aligned and the chunking fits, else the y-domain

@@ -61,6 +61,7 @@
 // Rows are bitwise independent of the batch size: the geometry depends on
 // (L, M, K) only.
 #include <algorithm>
+#include <cstring>
 
 #include "cascade.h"
 
@@ -70,9 +71,11 @@ namespace {
 constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
+constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 constexpr uint32_t kMaxSpins = 1u << 23;  // x s_sleep 2 (128 clk): ~0.4 s
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Padded LDS image of the tile's x window: 4 floats after every 32, so lane l's
 // window (x offset 32 l) starts at float 36 l; the 64 lanes' ds_read_b128 then
@@ -83,50 +86,62 @@ template <int L_, int M_, int TT_, int CR_>
 struct TileGeo {
   static constexpr int L = L_, M = M_, TT = TT_, CR = CR_;
   static_assert((kLS * L) % M == 0, "32 input samples per sub-chunk must make whole outputs");
+  static_assert(M % 2 == 0, "packed taps: windows of one branch share their x parity");
   static constexpr int TSUB = kLS * L / M;   // outputs per lane
   static constexpr int TILE = kWave * TSUB;  // outputs per workgroup
-  static_assert(TSUB % 8 == 0 && TSUB <= kWave, "two float4 halves; prep lanes");
+  static_assert(TSUB % 12 == 0 && TSUB <= kWave, "SRC in parts of 12; two float4 halves");
+  static constexpr int NP = TT / 2 + 1;      // tap pairs per branch
+  static_assert(NP <= kNPMax, "tap pairs");
   static constexpr int qi(int i) { return (i * M + CR) / L; }
   static constexpr int phi(int i) { return (i * M + CR) % L; }
-  static constexpr int W = qi(TSUB - 1) + TT;                       // lane window
+  // Output i sums taps u = -a .. 2 NP - 1 - a against x[qi + u] in pairs of
+  // (even, odd) x indices, a = qi mod 2: its pairs start at x index qs(i).
+  static constexpr int qs(int i) { return qi(i) & ~1; }
+  static constexpr int W = qs(TSUB - 1) + 2 * NP;                   // lane window
   static constexpr int NWIN = (kLS * (kWave - 1) + W + 3) / 4 * 4;  // tile window
   static constexpr int XF = xpad(NWIN + 4) + 4;                     // x image (floats)
   static constexpr int RS = TSUB + 4;                               // staging row stride
   static constexpr int SF = (kWave / 2) * RS;                       // staging (floats)
   static constexpr int CF = (kWave + 1) * kD * 2;                   // scan slots (floats)
   static constexpr int LDSF = XF > SF ? (XF > CF ? XF : CF) : (SF > CF ? SF : CF);
-  static constexpr int TB = TT * 4;  // tap bank: [u][phase], phase padded to 4
-  static_assert(L <= 4, "one float4 of taps per tap index");
+  static_assert(L <= 4, "four branch slots per tap pair row");
+  static_assert(qs(TSUB - 1) < W, "");
 };
 
-// Block-diagonal carry tables, float64, in the workspace (k_tile_prep).
-struct ModalTables {
-  double G[64][kD];        // G'[i], i < TSUB
+// Per-branch x parity of the windows (-1: no output of the sub-chunk uses the
+// branch); every output of a branch must share it (M even makes it so).
+template <class GEO>
+constexpr int branch_parity(int ph) {
+  int a = -1;
+  for (int i = 0; i < GEO::TSUB; ++i)
+    if (GEO::phi(i) == ph) {
+      const int ai = GEO::qi(i) & 1;
+      if (a >= 0 && a != ai) return -2;
+      a = ai;
+    }
+  return a;
+}
+
+// Tables of the single-pass kernel, built on the host in float64
+// (dsp_chain_tile_tables) and read by the kernel through the scalar cache.
+struct TileTables {
+  double G[64][kD];        // G'[i] = T^-1 A^(TSUB-1-i) B, i < TSUB (block-diagonal coords)
   double Dp[6][kS][4];     // D_k^(TSUB 2^d), row-major 2x2, d = 0..5
   double T[kD][kD];        // s = T m (row-major; zero rows/cols: padding stages)
-};
-
-// Kernel argument of k_tile_prep: B' = T^-1 B and the diagonal blocks, from
-// which it builds G'; the powers and T are copied as they are.
-struct ModalSeed {
-  double Bp[kD];
-  double Dk[kS][4];
-  double Dp[6][kS][4];
-  double T[kD][kD];
-  int tsub;
+  float TP[kNPMax][4][2];  // tap pairs: TP[p][ph] = (h[2p - a_ph], h[2p + 1 - a_ph])
+  int32_t tsub, np, L, M, K, S;  // what the tables were built for (checked at launch)
 };
 
 struct TileArgs {
   const float* x;
   float* y;
   float* z;
-  const float* taps;        // float32 L*h[K]
-  const ModalTables* mt;    // in the workspace
+  const TileTables* tt;     // device copy of dsp_chain_tile_tables' output
   double* states;           // [B][ntiles][12] tile end states (block-diagonal coords)
   uint32_t* flags;          // [B][ntiles]
   uint32_t* err;            // set when a hand-off wait gave up
   int64_t B, n_in, ld_x, n_out, ld_y, ntiles, cq;
-  int K, clip;
+  int clip;
   SosParams p;
 };
 
@@ -175,38 +190,40 @@ __device__ __forceinline__ void store_state(double* p, double v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+typedef __attribute__((address_space(4))) const TileTables* tt_ptr;
+
 // SRC outputs H0 .. H0+NH-1 of the lane's sub-chunk from its window at xw
-// (padded LDS image).  Per output: u ascending from 0, fmaf(tap, x, acc) --
-// k_src_reg's order, so the float32 results are bitwise the same.
+// (padded LDS image), two taps per v_pk_fma_f32: output i keeps the partial
+// sums of its even- and odd-indexed x samples in the halves of one register
+// pair, pairs p ascending, and y = even + odd -- the summation order of
+// k_src_reg's packed path (src_poly.hip), so y is bitwise the SRC kernel's.
 template <class GEO, int H0, int NH>
-__device__ __forceinline__ void src_part(const float* xw, const float* bank,
-                                         float (&y)[GEO::TSUB]) {
-  constexpr int V0 = GEO::qi(H0) / 4 * 4;
-  constexpr int V1 = GEO::qi(H0 + NH - 1) + GEO::TT;
+__device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[GEO::TSUB]) {
+  constexpr int V0 = GEO::qs(H0) / 4 * 4;
+  constexpr int V1 = GEO::qs(H0 + NH - 1) + 2 * GEO::NP;
   constexpr int NV = (V1 - V0 + 3) / 4 * 4;
-  float w[NV];
+  f32x2 w[NV / 2];
 #pragma unroll
   for (int k = 0; k < NV / 4; ++k) {
-    const int v = V0 + 4 * k;
-    const float4 f = *reinterpret_cast<const float4*>(xw + xpad(v));
-    w[4 * k + 0] = f.x;
-    w[4 * k + 1] = f.y;
-    w[4 * k + 2] = f.z;
-    w[4 * k + 3] = f.w;
+    const f32x4 f = *reinterpret_cast<const f32x4*>(xw + xpad(V0 + 4 * k));
+    w[2 * k] = f32x2{f.x, f.y};
+    w[2 * k + 1] = f32x2{f.z, f.w};
   }
-  float acc[NH];
+  f32x2 acc[NH];
 #pragma unroll
-  for (int i = 0; i < NH; ++i) acc[i] = 0.f;
+  for (int i = 0; i < NH; ++i) acc[i] = f32x2{0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < GEO::TT; ++u) {
-    const float4 t4 = *reinterpret_cast<const float4*>(bank + 4 * u);  // broadcast
-    const float tp[4] = {t4.x, t4.y, t4.z, t4.w};
+  for (int p = 0; p < GEO::NP; ++p) {
+    f32x2 t[GEO::L];
+#pragma unroll
+    for (int ph = 0; ph < GEO::L; ++ph) t[ph] = f32x2{tt->TP[p][ph][0], tt->TP[p][ph][1]};
 #pragma unroll
     for (int i = 0; i < NH; ++i)
-      acc[i] = fmaf(tp[GEO::phi(H0 + i)], w[GEO::qi(H0 + i) - V0 + u], acc[i]);
+      acc[i] = __builtin_elementwise_fma(t[GEO::phi(H0 + i)],
+                                         w[(GEO::qs(H0 + i) - V0) / 2 + p], acc[i]);
   }
 #pragma unroll
-  for (int i = 0; i < NH; ++i) y[H0 + i] = acc[i];
+  for (int i = 0; i < NH; ++i) y[H0 + i] = acc[i].x + acc[i].y;
 }
 
 // Stores the tile's 64 x TSUB outputs (lane l holds outputs l*TSUB + i) as
@@ -254,20 +271,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     TileArgs a) {
   constexpr int TS = GEO::TSUB;
   __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
-  __shared__ __attribute__((aligned(16))) float bank[GEO::TB];
   const int lane = threadIdx.x;
   const int64_t id = blockIdx.x;
   const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
   const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
-  typedef __attribute__((address_space(4))) const ModalTables* mt_ptr;
-  const mt_ptr mt = (mt_ptr)a.mt;  // wave-uniform: scalar loads
+  const tt_ptr mt = (tt_ptr)a.tt;  // wave-uniform: scalar loads
 
-  // ---- tap bank: bank[u][ph] = taps[ph + L*(TT-1-u)] (0 past K): tap u of
-  // branch ph in the reversed order the SRC sums in.
-  for (int i = lane; i < GEO::TB; i += kWave) {
-    const int u = i >> 2, ph = i & 3, k = ph + GEO::L * (GEO::TT - 1 - u);
-    bank[i] = (ph < GEO::L && k < a.K) ? a.taps[k] : 0.f;
-  }
   // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
   {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -280,20 +289,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
       if ((k + 1) * kWave <= NF || f < NF) {
         // "Negative" offsets (tile 0) are >= 2^31 as unsigned: out of range, zeros.
         const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, 0);
-        *reinterpret_cast<float4*>(lds + xpad(4 * f)) = make_float4(v.x, v.y, v.z, v.w);
+        *reinterpret_cast<f32x4*>(lds + xpad(4 * f)) = v;
       }
     }
   }
   fence();  // one wave: its LDS operations execute in order
 
-  // ---- 1. SRC: the lane's TSUB outputs, in two halves (register pressure)
+  // ---- 1. SRC: the lane's TSUB outputs, in parts of 12 (register pressure)
   float y[TS];
   {
     const float* xw = lds + 36 * lane;
-    src_part<GEO, 0, TS / 2>(xw, bank, y);
+    static_assert(TS == 48, "four parts");
+    src_part<GEO, 0, 12>(xw, mt, y);
     pin(y);
-    fence();
-    src_part<GEO, TS / 2, TS / 2>(xw, bank, y);
+    src_part<GEO, 12, 12>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 24, 12>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 36, 12>(xw, mt, y);
     pin(y);
   }
 
@@ -407,26 +420,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   store_tile<GEO>(lds, y, lane_z, rz, m0);
 }
 
-// Block-diagonal tables into the workspace: lane i < tsub builds
-// G'[i] = D^(tsub-1-i) B' (2x2 block powers), the rest is copied.
-__global__ __launch_bounds__(kWave) void k_tile_prep(ModalSeed sd, ModalTables* mt) {
-  const int i = threadIdx.x;
-  if (i < sd.tsub) {
-    double g[kD];
-    for (int d = 0; d < kD; ++d) g[d] = sd.Bp[d];
-    for (int s = 0; s < sd.tsub - 1 - i; ++s)
-      for (int k = 0; k < kS; ++k) {
-        const double* M = sd.Dk[k];
-        const double g0 = g[2 * k], g1 = g[2 * k + 1];
-        g[2 * k] = M[0] * g0 + M[1] * g1;
-        g[2 * k + 1] = M[2] * g0 + M[3] * g1;
-      }
-    for (int d = 0; d < kD; ++d) mt->G[i][d] = g[d];
-  }
-  for (int j = i; j < 6 * kS * 4; j += kWave) (&mt->Dp[0][0][0])[j] = (&sd.Dp[0][0][0])[j];
-  for (int j = i; j < kD * kD; j += kWave) (&mt->T[0][0])[j] = (&sd.T[0][0])[j];
-}
-
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
 typedef TileGeo<3, 2, 41, 0> Geo3241;
@@ -479,10 +472,10 @@ bool solve4(double M[4][4], double r[4]) {
 }
 
 // Block-diagonal form of the first 2*Sr states (the real stages): T block
-// unit lower triangular with A T = T D, D = diag(A_kk).  Fills the kernel's
-// seed (G' generator B' = T^-1 B, D blocks and their powers, T); false when
-// two stages share a pole pair or T is ill-conditioned.
-bool modal_seed(const SosParams& p, int Sr, int tsub, ModalSeed* sd) {
+// unit lower triangular with A T = T D, D = diag(A_kk).  Fills the carry part
+// of the tables (G' = D^(tsub-1-i) B' with B' = T^-1 B, the powers of D, T);
+// false when two stages share a pole pair or T is ill-conditioned.
+bool modal_tables(const SosParams& p, int Sr, int tsub, TileTables* tt) {
   const int n = 2 * Sr;
   const std::vector<double> A = state_matrix(p, kS);  // 12 x 12
   auto Aat = [&](int r, int c) { return A[(size_t)r * kD + c]; };
@@ -537,52 +530,77 @@ bool modal_seed(const SosParams& p, int Sr, int tsub, ModalSeed* sd) {
   }
   if (!(nT * nTi < 1e8)) return false;
   // B of the realisation (includes the input gain), then B' = T^-1 B.
-  double Bv[kD] = {0};
+  double Bv[kD] = {0}, Bp[kD];
   cascade_state_step(p, kS, true, Bv, 1.0);
   for (int r = 0; r < kD; ++r) {
     double s = 0.0;
     for (int c = 0; c < n; ++c) s += Ti[(size_t)r * kD + c] * Bv[c];
-    sd->Bp[r] = r < n ? s : 0.0;
+    Bp[r] = r < n ? s : 0.0;
   }
+  auto mul = [](const double* X, const double* Y, double* Z) {
+    const double z0 = X[0] * Y[0] + X[1] * Y[2], z1 = X[0] * Y[1] + X[1] * Y[3];
+    const double z2 = X[2] * Y[0] + X[3] * Y[2], z3 = X[2] * Y[1] + X[3] * Y[3];
+    Z[0] = z0;
+    Z[1] = z1;
+    Z[2] = z2;
+    Z[3] = z3;
+  };
   for (int k = 0; k < kS; ++k) {
     double Dk[4] = {0, 0, 0, 0};
     if (k < Sr)
       for (int q = 0; q < 4; ++q) Dk[q] = Aat(2 * k + q / 2, 2 * k + q % 2);
-    for (int q = 0; q < 4; ++q) sd->Dk[k][q] = Dk[q];
+    // G'[i] block k = D_k^(tsub-1-i) B'_k, from i = tsub-1 down.
+    double g0 = Bp[2 * k], g1 = Bp[2 * k + 1];
+    for (int i = tsub - 1; i >= 0; --i) {
+      tt->G[i][2 * k] = g0;
+      tt->G[i][2 * k + 1] = g1;
+      const double n0 = Dk[0] * g0 + Dk[1] * g1, n1 = Dk[2] * g0 + Dk[3] * g1;
+      g0 = n0;
+      g1 = n1;
+    }
     // D_k^tsub by square-and-multiply, then repeated squaring per level.
     double R[4] = {1, 0, 0, 1}, Bq[4] = {Dk[0], Dk[1], Dk[2], Dk[3]};
-    auto mul = [](const double* X, const double* Y, double* Z) {
-      const double z0 = X[0] * Y[0] + X[1] * Y[2], z1 = X[0] * Y[1] + X[1] * Y[3];
-      const double z2 = X[2] * Y[0] + X[3] * Y[2], z3 = X[2] * Y[1] + X[3] * Y[3];
-      Z[0] = z0;
-      Z[1] = z1;
-      Z[2] = z2;
-      Z[3] = z3;
-    };
     for (int e = tsub; e > 0; e >>= 1) {
       if (e & 1) mul(R, Bq, R);
       if (e > 1) mul(Bq, Bq, Bq);
     }
     for (int d = 0; d < 6; ++d) {
-      for (int q = 0; q < 4; ++q) sd->Dp[d][k][q] = k < Sr ? R[q] : 0.0;
+      for (int q = 0; q < 4; ++q) tt->Dp[d][k][q] = k < Sr ? R[q] : 0.0;
       mul(R, R, R);
     }
   }
   for (int r = 0; r < kD; ++r)
-    for (int c = 0; c < kD; ++c) sd->T[r][c] = (r < n && c < n) ? T[(size_t)r * kD + c] : 0.0;
-  sd->tsub = tsub;
+    for (int c = 0; c < kD; ++c) tt->T[r][c] = (r < n && c < n) ? T[(size_t)r * kD + c] : 0.0;
   return true;
 }
 
+// Tap pairs of the packed SRC: branch ph, pair p = (h[2p - a], h[2p + 1 - a])
+// with h[u] = taps[ph + L (TT - 1 - u)] (0 outside [0, TT) or past K) and a the
+// branch's window parity.
+template <class GEO>
+void tap_pairs(const float* taps, int K, TileTables* tt) {
+  for (int p = 0; p < kNPMax; ++p)
+    for (int ph = 0; ph < 4; ++ph)
+      for (int e = 0; e < 2; ++e) {
+        float v = 0.f;
+        const int a = ph < GEO::L ? branch_parity<GEO>(ph) : -1;
+        if (a >= 0 && p < GEO::NP) {
+          const int u = 2 * p + e - a;
+          const int k = ph + GEO::L * (GEO::TT - 1 - u);
+          if (u >= 0 && u < GEO::TT && k < K) v = taps[k];
+        }
+        tt->TP[p][ph][e] = v;
+      }
+}
+
 struct TileWs {
-  size_t err_off, g_off, st_off, fl_off, total;
+  size_t err_off, st_off, fl_off, total;
 };
 
-TileWs tile_ws(int64_t B, int64_t ntiles, int64_t tsub) {
+TileWs tile_ws(int64_t B, int64_t ntiles) {
   TileWs w;
   w.err_off = 0;  // include/dspcore.h: the workspace's first word
-  w.g_off = 256;  // ModalTables
-  w.st_off = w.g_off + align256(sizeof(ModalTables));
+  w.st_off = 256;
   w.fl_off = w.st_off + align256((size_t)B * ntiles * kD * sizeof(double));
   w.total = w.fl_off + align256((size_t)B * ntiles * sizeof(uint32_t));
   return w;
@@ -599,36 +617,59 @@ size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K,
                                   int64_t c, int S) {
   TilePlan tp;
   if (B <= 0 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 0;
-  return tile_ws(B, tp.ntiles, tp.tsub).total;
+  return tile_ws(B, tp.ntiles).total;
+}
+
+size_t chain_tile_tables_bytes() { return sizeof(TileTables); }
+
+int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, const float* taps,
+                      int K, int L, int M, int64_t c, const double* sos, int S) {
+  TilePlan tp;
+  if (!tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
+  DSP_REQUIRE(out && out_bytes >= sizeof(TileTables), "tables buffer too small: %zu < %zu bytes",
+              out_bytes, sizeof(TileTables));
+  DSP_REQUIRE(taps && (S == 0 || sos), "null pointer");
+  SosParams p;
+  if (S > 0 && !realize(sos, S, &p)) return kNotFused;  // a b0 == 0 band: no NORM form
+  if (S == 0) realize(nullptr, 0, &p);
+  TileTables* tt = static_cast<TileTables*>(out);
+  std::memset(tt, 0, sizeof(TileTables));
+  if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
+  tap_pairs<Geo3241>(taps, K, tt);
+  tt->tsub = (int32_t)tp.tsub;
+  tt->np = Geo3241::NP;
+  tt->L = L;
+  tt->M = M;
+  tt->K = K;
+  tt->S = S;
+  return DSP_OK;
 }
 
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
-                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
-                      int64_t c, const double* sos, int S, int clip, void* ws, size_t ws_bytes,
-                      hipStream_t s) {
+                      int64_t n_out, int64_t ld_y, int K, int L, int M, int64_t c,
+                      const double* sos, int S, int clip, const void* tables, void* ws,
+                      size_t ws_bytes, hipStream_t s) {
   TilePlan tp;
-  if (!tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
+  if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
   auto aligned = [](const void* p, int64_t ld) {
     return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   };
   if (!aligned(x, ld_x) || !aligned(y, ld_y) || !aligned(z, ld_y)) return kNotFused;
   SosParams p;
-  if (S > 0 && !realize(sos, S, &p)) return kNotFused;  // a b0 == 0 band: no NORM form
+  if (S > 0 && !realize(sos, S, &p)) return kNotFused;
   if (S == 0) realize(nullptr, 0, &p);
-  ModalSeed sd;
-  if (!modal_seed(p, S, (int)tp.tsub, &sd)) return kNotFused;  // shared poles: two-launch
-  const TileWs w = tile_ws(B, tp.ntiles, tp.tsub);
+  const TileWs w = tile_ws(B, tp.ntiles);
   DSP_REQUIRE(ws && ws_bytes >= w.total, "chain workspace too small: %zu < %zu bytes", ws_bytes,
               w.total);
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 255) == 0, "chain workspace not 256-B aligned");
+  DSP_REQUIRE((reinterpret_cast<uintptr_t>(tables) & 255) == 0, "chain tables not 256-B aligned");
   DSP_REQUIRE(B * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
   char* base = static_cast<char*>(ws);
   TileArgs a;
   a.x = x;
   a.y = y;
   a.z = z;
-  a.taps = taps;
-  a.mt = reinterpret_cast<const ModalTables*>(base + w.g_off);
+  a.tt = static_cast<const TileTables*>(tables);
   a.states = reinterpret_cast<double*>(base + w.st_off);
   a.flags = reinterpret_cast<uint32_t*>(base + w.fl_off);
   a.err = reinterpret_cast<uint32_t*>(base + w.err_off);
@@ -639,15 +680,8 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.ld_y = ld_y;
   a.ntiles = tp.ntiles;
   a.cq = c / L;
-  a.K = K;
   a.clip = clip;
   a.p = p;
-  {
-    TraceScope trace("chain_prep", s);
-    hipLaunchKernelGGL(k_tile_prep, dim3(1), dim3(kWave), 0, s, sd,
-                       reinterpret_cast<ModalTables*>(base + w.g_off));
-  }
-  DSP_LAUNCHED("k_tile_prep");
   {
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,

@@ -17,7 +17,7 @@
 //
 // The register-blocked kernel is the standalone SRC and the two-launch chain's
 // first kernel; the chain's default path computes the same outputs inside its
-// single-pass kernel (chain_tile.hip), with the same per-output FMA order.
+// single-pass kernel (chain_tile.hip), in the same summation order.
 #include "common.h"
 
 namespace dsp {
@@ -68,20 +68,34 @@ __device__ __forceinline__ void store_tile(float* __restrict__ yr,
 // one polyphase branch phi, and their input windows are shifted by M samples,
 // so one tap read feeds R FMAs and one window read feeds up to T FMAs:
 // (T + (R-1)M) + T LDS reads per R*T FMAs.
+//
+// For even M every window of a thread starts at the same x parity a, and the
+// sum runs two taps per v_pk_fma_f32: the halves of one register pair keep the
+// partial sums over the even- and odd-indexed x samples, pair p covering
+// x[E + 2p], x[E + 2p + 1] from the even start E = Q - a (Q = q - (T-1), the
+// window start) against taps (h[2p - a], h[2p + 1 - a]), h[u] = P[phi][T-1-u]
+// (0 outside [0, T)); y = even + odd.  This is the canonical summation order
+// of the SRC for even M; the single-pass chain kernel (chain_tile.hip) uses
+// it too, so both produce bitwise the same y.  Odd M sums the taps in order.
 // ---------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int L, int M, int T, int R, int NT>
 __global__ __launch_bounds__(NT) void k_src_reg(
     const float* __restrict__ x, float* __restrict__ y, int64_t n_in,
     int64_t ld_x, int64_t n_out, int64_t ld_y, const float* __restrict__ taps,
     int K, int64_t c, int vec_x, int vec_y) {
+  constexpr bool PACK = M % 2 == 0;
   constexpr int G = NT / L;          // thread groups with one thread per phase
   constexpr int TILE = G * L * R;    // outputs per block
-  constexpr int TP = ((T + 3) / 4) * 4 + 4;               // padded bank row
+  constexpr int NP = T / 2 + 1;                           // tap pairs (packed)
+  constexpr int TP = PACK ? ((2 * NP + 3) / 4) * 4 : ((T + 3) / 4) * 4 + 4;  // bank row
+  constexpr int NROW = PACK ? 2 * L : L;                  // rows: (phi, a) or phi
   constexpr int WMAX = ((TILE - 1) * M) / L + T + 2 + 8;  // window + align slack
   constexpr int WF = ((WMAX + 3) / 4) * 4;
   static_assert(TILE % 4 == 0, "tile must be float4 aligned");
 
-  __shared__ __attribute__((aligned(16))) float s_bank[L * TP];
+  __shared__ __attribute__((aligned(16))) float s_bank[NROW * TP];
   __shared__ __attribute__((aligned(16))) float s_win[WF];
   __shared__ __attribute__((aligned(16))) float s_out[TILE];
 
@@ -94,13 +108,16 @@ __global__ __launch_bounds__(NT) void k_src_reg(
   const int64_t qlo = (m0 * M + c) / L - (T - 1);
   const int64_t qhi = ((m0 + TILE - 1) * M + c) / L;
   const int64_t qa = qlo & ~(int64_t)3;
-  load_window<NT>(s_win, xr, qa, (int)(qhi - qa + 1), n_in, vec_x != 0);
+  // Packed pairs reach up to 2 samples past the last window (zero taps there).
+  load_window<NT>(s_win, xr, qa, (int)(qhi - qa + 1 + (PACK ? 2 : 0)), n_in, vec_x != 0);
 
-  // Bank row phi holds the branch taps reversed: s_bank[phi][u] = P[phi][T-1-u].
-  for (int i = tid; i < L * TP; i += NT) {
-    const int phi = i / TP, u = i - phi * TP;
-    const int k = phi + L * (T - 1 - u);
-    s_bank[i] = (u < T && k < K) ? taps[k] : 0.f;
+  // Bank row phi holds the branch taps reversed, h[u] = P[phi][T-1-u]; the
+  // packed bank has one row per (phi, a): row[k] = h[k - a].
+  for (int i = tid; i < NROW * TP; i += NT) {
+    const int row = i / TP, k = i - row * TP;
+    const int phi = PACK ? row >> 1 : row, u = PACK ? k - (row & 1) : k;
+    const int kk = phi + L * (T - 1 - u);
+    s_bank[i] = (u >= 0 && u < T && kk < K) ? taps[kk] : 0.f;
   }
   __syncthreads();
 
@@ -110,19 +127,38 @@ __global__ __launch_bounds__(NT) void k_src_reg(
     const int64_t j = (m0 + lbase) * M + c;
     const int64_t q = j / L;
     const int phi = (int)(j - q * L);
-    const float* w = s_win + (int)(q - (T - 1) - qa);
-    const float* h = s_bank + phi * TP;
-    float acc[R];
+    if constexpr (PACK) {
+      const int64_t Q = q - (T - 1);
+      const int a = (int)(Q & 1);
+      const f32x2* w = reinterpret_cast<const f32x2*>(s_win + (int)(Q - a - qa));
+      const f32x2* h = reinterpret_cast<const f32x2*>(s_bank + (2 * phi + a) * TP);
+      f32x2 acc[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+      for (int r = 0; r < R; ++r) acc[r] = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < T; ++u) {
-      const float t = h[u];
+      for (int u = 0; u < NP; ++u) {
+        const f32x2 t = h[u];
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(t, w[r * M + u], acc[r]);
+        for (int r = 0; r < R; ++r)
+          acc[r] = __builtin_elementwise_fma(t, w[r * (M / 2) + u], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r].x + acc[r].y;
+    } else {
+      const float* w = s_win + (int)(q - (T - 1) - qa);
+      const float* h = s_bank + phi * TP;
+      float acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int u = 0; u < T; ++u) {
+        const float t = h[u];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = fmaf(t, w[r * M + u], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r];
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r];
   }
   __syncthreads();
 

@@ -59,7 +59,10 @@ _SIGNATURES = {
     "dsp_chain_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,
-        _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+        _vp, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "dsp_chain_tile_tables_bytes": (_c_sz, []),
+    "dsp_chain_tile_tables": (ctypes.c_int, [_vp, _c_sz, _c_i64, _c_i64, _vp, _c_i32, _c_i32,
+                                             _c_i32, _c_i64, _dp, _c_i32]),
     "dsp_chain_path": (ctypes.c_int, [_c_i32]),
     "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,

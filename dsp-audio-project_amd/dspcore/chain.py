@@ -37,7 +37,11 @@ class Chain:
 
     def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
                  chunk_len: int | None = None, use_table: bool = True,
-                 use_xstate: bool = True):
+                 use_xstate: bool = True, plan_batch: int | None = None):
+        """plan_batch: the batch size the cascade's chunking is planned for
+        (default: `batch`).  Shards of one job pass the job's total batch so
+        that every shard runs the same chunking and the rows come out bitwise
+        equal to the unsharded run (design.max_chunks_for)."""
         ops.require_gpu()
         self.cfg = cfg
         self.B = int(batch)
@@ -59,7 +63,7 @@ class Chain:
         # Two-launch path (other geometries, or dsp_chain_path(1)): x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
         # the row into far fewer chunks than the plain rule.
-        mc = max_chunks_for(self.B)
+        mc = max_chunks_for(self.B if plan_batch is None else int(plan_batch))
         plain = chunk_len_for(n_out, mc)
         eligible = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
                     and 1 <= S <= 8 and S != 7)
@@ -86,6 +90,23 @@ class Chain:
         # and every completed call leaves them clear (include/dspcore.h).
         self.workspace = torch.zeros(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
         self.table = ops.state_table(self.sos, self.chunk_len, dev) if use_table else None
+        # Single-pass kernel tables (dsp_chain_tile_tables): built once on the
+        # host in float64 from the float32 taps and the sos, kept on the device.
+        self.tile_tables = None
+        if self.tile_len > 0:
+            nbytes = int(lib.dsp_chain_tile_tables_bytes())
+            host = np.zeros(nbytes, dtype=np.uint8)
+            taps32 = np.ascontiguousarray(self.src.taps, dtype=np.float32)
+            rc = lib.dsp_chain_tile_tables(
+                host.ctypes.data, nbytes, cfg.n_in, n_out, taps32.ctypes.data, self.src.K,
+                self.src.L, self.src.M, self.src.c_offset, _lib.sos_pointer(self.sos), S)
+            if rc < 0:
+                _lib.check(rc, "dsp_chain_tile_tables")
+            if rc == 0:
+                # 256-byte aligned device copy (torch's allocator aligns to 512 B)
+                self.tile_tables = torch.from_numpy(host).to(dev)
+            else:
+                self.tile_len = 0
         self.xtable, self.xrows = (ops.xstate_table(self.sos, self.src, self.chunk_len, dev)
                                    if self.xstate else (None, 0))
 
@@ -125,7 +146,7 @@ class Chain:
                 self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.y),
                 self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
                 sos_ptr, S, clip, self.chunk_len, ops._ptr(self.table), ops._ptr(self.xtable),
-                self.xrows, self.spec.seg_start, self.spec.seg_len,
+                self.xrows, ops._ptr(self.tile_tables), self.spec.seg_start, self.spec.seg_len,
                 self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)

@@ -4,8 +4,15 @@ Channels never interact, so a batch is cut into contiguous channel ranges of
 ceil(B/g) rows, one per device; each device gets its own copy of the LUTs and
 runs the same kernels on its own stream from its own host thread (ctypes drops
 the GIL while the ABI runs).  No collective, no device-to-device traffic: the
-per-device results are gathered on the host.  Because the kernels' results do
-not depend on the batch size, the output is bitwise identical for any g.
+per-device results are gathered on the host.
+
+Bitwise invariance: no kernel's arithmetic depends on the batch size, only on
+the plan.  The single-pass chain kernel's geometry depends on (L, M, K) only;
+the two-launch cascade's chunk length depends on the batch the chain is
+planned for (design.max_chunks_for: <= 64 chunks from 2048 channels, <= 256
+below), so shards must plan with the job's total batch
+(`Chain(..., plan_batch=B_total)`, as bench.py does) to be bitwise equal to the
+unsharded run; planned per shard they agree to float64 rounding only.
 """
 from __future__ import annotations
 

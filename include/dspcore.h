@@ -154,14 +154,25 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero (today:
  * (L, M, ceil(K/L)) = (3, 2, 41) with c_offset mod 3 == 0 and
  * (c_offset/3 - 40) mod 4 == 0, S <= 6 with every b0 != 0, n_in and n_out
- * multiples of 4) and the rows of x, y and z are 16-byte aligned with pitches
- * that are multiples of 4, ONE kernel computes y and z from x: x is read once,
- * y and z are written once, y is never read back.  Its y is bitwise that of
+ * multiples of 4), `tile_tables` is a device copy (256-byte aligned) of the
+ * tables dsp_chain_tile_tables built for this call's geometry, taps and sos,
+ * and the rows of x, y and z are 16-byte aligned with pitches that are
+ * multiples of 4, ONE kernel computes y and z from x: x is read once, y and z
+ * are written once, y is never read back.  Its y is bitwise that of
  * dsp_src_polyphase_f32; z equals the two-launch chain's to float64 rounding.
- * It derives its own state tables from sos_host (chunk_len, state_table and
- * xstate_table are not used).  Workspace word 0 (uint32) is nonzero after a
- * call whose tile hand-off wait gave up (a broken dispatch order; z is then
- * wrong): a diagnostic, normally 0.
+ * chunk_len, state_table and xstate_table are not used by it.  Workspace word
+ * 0 (uint32) is nonzero after a call whose tile hand-off wait gave up (a broken
+ * dispatch order; z is then wrong): a diagnostic, normally 0.
+ *
+ * dsp_chain_tile_tables (HOST, no device work) fills `tables_host`
+ * (>= dsp_chain_tile_tables_bytes()) with the single-pass kernel's float64
+ * carry tables (the cascade in block-diagonal coordinates: the sub-chunk
+ * state-response rows, the powers of the diagonal blocks, the change of basis)
+ * and its packed tap pairs, from the HOST float32 taps (the same values as
+ * `taps`) and sos.  Returns 0 when the single-pass kernel serves the geometry
+ * (copy the buffer to the device once and pass it to every call), 1 when it
+ * does not (the two-launch path serves it; nothing to copy), DSP_EINVAL on bad
+ * arguments.  With tile_tables == NULL dsp_chain_f32 takes the two-launch path.
  *
  * Two-launch path (any other geometry, or dsp_chain_path(1)): SRC, then the
  * cascade.  With `xstate_table` (device, float64 [xstate_rows][2S], may be
@@ -187,6 +198,10 @@ int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, in
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t K,
                                  int32_t L, int32_t M, int64_t c_offset, int32_t S,
                                  int64_t chunk_len);
+size_t dsp_chain_tile_tables_bytes(void);
+int dsp_chain_tile_tables(void* tables_host, size_t tables_bytes, int64_t n_in, int64_t n_out,
+                          const float* taps_host, int32_t K, int32_t L, int32_t M,
+                          int64_t c_offset, const double* sos_host, int32_t S);
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
                               int64_t c_offset, int64_t* shift, int64_t* q0,
                               int64_t* rows);
@@ -196,7 +211,7 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
                   const double* xstate_table, int64_t xstate_rows,
-                  int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  const void* tile_tables, int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
                   size_t workspace_bytes, void* stream);
 

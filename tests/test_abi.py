@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 22
+    assert len(names) == 24
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -153,3 +153,57 @@ def test_chain_path_tile_len_and_workspace_query():
     ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)
     assert ws >= B * tiles * (12 * 8 + 4)
     assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 1023, 160, 147, 511, 6, 1152) == 0
+
+
+def test_chain_tile_tables_host_only():
+    """dsp_chain_tile_tables (host, no GPU) for config 3's geometry: the
+    block-diagonal carry tables reproduce the cascade's dense state algebra
+    (T D^(48 2^d) T^-1 = A^(48 2^d); T sum_i G'[i] y[i] = the zero-state end
+    state of a 48-sample sub-chunk) and the tap pairs are the reversed
+    polyphase branches shifted by their window parity; other geometries
+    decline with 1."""
+    import numpy as np
+
+    from dspcore import design
+    lib = _lib.load()
+    gains = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3,
+             "Presence": 5, "Brilliance": -6}
+    plan = design.src_plan(48000, 48000, 2, 3)
+    sos = np.ascontiguousarray(design.eq_plan(72000, gains).sos)
+    nbytes = lib.dsp_chain_tile_tables_bytes()
+    assert nbytes == 64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4
+    buf = np.zeros(nbytes, np.uint8)
+    taps32 = np.ascontiguousarray(plan.taps, dtype=np.float32)
+    rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, 72000, taps32.ctypes.data,
+                                   plan.K, 3, 2, plan.c_offset, _lib.sos_pointer(sos), 6)
+    assert rc == 0
+    G = buf[:6144].view(np.float64).reshape(64, 12)
+    Dp = buf[6144:7296].view(np.float64).reshape(6, 6, 2, 2)
+    T = buf[7296:8448].view(np.float64).reshape(12, 12)
+    TP = buf[8448:9472].view(np.float32).reshape(32, 4, 2)
+    assert tuple(buf[9472:].view(np.int32)) == (48, 21, 3, 2, 121, 6)
+    A, B = design.state_space(sos)
+    Ti = np.linalg.inv(T)
+    for d in range(6):
+        D = np.zeros((12, 12))
+        for k in range(6):
+            D[2 * k:2 * k + 2, 2 * k:2 * k + 2] = Dp[d, k]
+        An = np.linalg.matrix_power(A, 48 << d)
+        np.testing.assert_allclose(T @ D @ Ti, An, atol=1e-9 * max(1.0, np.abs(An).max()))
+    y = np.random.default_rng(0).uniform(-1, 1, 48)
+    X = np.zeros(12)
+    for v in y:
+        X = A @ X + B * v
+    np.testing.assert_allclose(T @ (G[:48].T @ y), X, rtol=1e-10, atol=1e-12)
+    # tap pairs: branch ph, pair p = (h[2p - a], h[2p + 1 - a]), h[u] = taps[ph + 3 (40 - u)]
+    for ph in range(3):
+        a = [((2 * i) // 3) & 1 for i in range(48) if (2 * i) % 3 == ph][0]
+        h = np.array([taps32[ph + 3 * (40 - u)] if 0 <= u < 41 and ph + 3 * (40 - u) < 121
+                      else 0.0 for u in range(-1, 43)], dtype=np.float32)
+        want = np.array([[h[2 * p - a + 1], h[2 * p + 2 - a]] for p in range(21)])
+        np.testing.assert_array_equal(TP[:21, ph], want)
+    assert not TP[21:].any() and not TP[:, 3].any()
+    c5 = design.src_plan(48000, 44100, 147, 160, 1023)
+    t5 = np.ascontiguousarray(c5.taps, dtype=np.float32)
+    assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c5.n_out, t5.ctypes.data,
+                                     c5.K, 160, 147, c5.c_offset, _lib.sos_pointer(sos), 6) == 1

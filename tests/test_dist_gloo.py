@@ -1,6 +1,7 @@
 """The N > 1 bench path on CPU: two gloo ranks run bench.timed_loop (barrier +
 sync bracketing, max-over-ranks of the elapsed time) and the channel-shard
-bookkeeping.  The GPU-side RCCL launch of bench.py uses the same harness."""
+bookkeeping (config 4's 32768 channels: 16384 per rank).  bench.py's GPU
+ranks use the same harness over gloo too (no RCCL)."""
 import os
 import socket
 import time
@@ -34,6 +35,7 @@ def _worker(rank, world, port, out):
 
         elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, dist=dist)
         lo, hi = shard_ranges(32768, world)[rank]
+        assert bench.rank_channels(bench.WORKLOADS["c4"]["channels"], rank, world) == (lo, hi)
         out[rank] = (elapsed, len(calls), lo, hi)
     finally:
         dist.destroy_process_group()

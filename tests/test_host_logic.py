@@ -206,34 +206,3 @@ def test_bluestein_tables_compute_the_dft():
         d = np.fft.fft(np.conj(np.fft.fft(a) * bf))
         got = chirp * np.conj(d[:n])
         assert np.max(np.abs(got - np.fft.fft(x))) <= 1e-12 * max(1.0, np.max(np.abs(got)))
-
-
-def test_src_emitted_chunk_states_algebra():
-    """Chain mode 2 (csrc/src_poly.hip emit_states, restated in numpy):
-    sub-chunk states with the last 96 rows of G, carried to the chunk end by
-    Horner steps with A^96 and split over SRC tiles of 2880 outputs (the two
-    pieces of a chunk summed), equal the chunk end state sum_t G[t] y[cT + t]
-    of the cascade's own first pass."""
-    U, TILE = 96, 2880
-    gains = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3,
-             "Presence": 5, "Brilliance": -6}
-    sos = design.eq_plan(72000, gains).sos
-    A, _ = design.state_space(sos)
-    AU = np.linalg.matrix_power(A, U)
-    rng = np.random.default_rng(5)
-    n = 3 * TILE + 500
-    y = rng.uniform(-1, 1, n).astype(np.float32).astype(np.float64)
-    for T in (288, 1152):
-        G = design.state_response_table(sos, T)
-        g = G[T - U:]
-        C = -(-n // T)
-        for c in range(C - 1):
-            ref = G.T @ y[c * T:(c + 1) * T]
-            got = np.zeros_like(ref)
-            for tile in range(c * T // TILE, (c * T + T - 1) // TILE + 1):
-                hi = min((c + 1) * T, (tile + 1) * TILE)
-                S = np.zeros_like(ref)
-                for j0 in range(max(c * T, tile * TILE), (c + 1) * T, U):
-                    S = AU @ S + (g.T @ y[j0:j0 + U] if j0 < hi else 0.0)
-                got += S
-            np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10 * np.abs(ref).max())

@@ -1,4 +1,9 @@
-"""Runs the config-3 chain a few times (for rocprofv3 --pmc passes)."""
+"""Runs a bench workload's chain a few times on cuda:0 (the program the
+rocprofv3 --pmc passes of tools/pmc_chain.sh profile).
+
+    python tools/kernels_once.py [reps] [config] [channels]
+    config: c3 (default) | c4 | c5, channels default the config's one-GPU batch.
+"""
 import os
 import sys
 
@@ -7,15 +12,19 @@ sys.path[:0] = [os.path.join(ROOT, "dsp-audio-project_amd"), ROOT]
 
 import torch  # noqa: E402
 
+import bench  # noqa: E402
 from dspcore.chain import Chain, ChainConfig  # noqa: E402
 
-gains = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3, "Presence": 5, "Brilliance": -6}
-cfg = ChainConfig(48000, 48000, 3, 2, None, gains, n_fft=4096)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+wl = bench.WORKLOADS[sys.argv[2] if len(sys.argv) > 2 else "c3"]
+B = int(sys.argv[3]) if len(sys.argv) > 3 else wl["channels"]
+cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], bench.CONFIG3_GAINS,
+                  n_fft=wl["n_fft"])
 dev = torch.device("cuda", 0)
-ch = Chain(cfg, 4096, dev)
-x = torch.rand((4096, 48000), device=dev) * 2 - 1
+ch = Chain(cfg, B, dev, plan_batch=wl["channels"])
+x = torch.rand((B, wl["n_in"]), device=dev) * 2 - 1
 for _ in range(reps):
     ch.run(x)
 torch.cuda.synchronize()
-print("done")
+assert ch.handoff_ok()
+print("done", wl["name"], B)
