@@ -224,9 +224,9 @@ int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double th
 }
 
 int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
-                       int64_t ld_out, uint32_t* peak_out, void* stream) {
+                       int64_t ld_out, uint32_t* peak_out, int32_t precision, void* stream) {
   dsp::clear_error();
-  return dsp::launch_quantize_pcm16(z, out, B, n, ld_z, ld_out, peak_out,
+  return dsp::launch_quantize_pcm16(z, out, B, n, ld_z, ld_out, peak_out, precision,
                                     static_cast<hipStream_t>(stream));
 }
 

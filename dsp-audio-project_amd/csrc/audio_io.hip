@@ -20,6 +20,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace dsp {
@@ -125,24 +127,30 @@ __global__ __launch_bounds__(kIoNT) void k_scale(float* __restrict__ x, int64_t 
     r[i] = r[i] / pk;
 }
 
+// app.py:349-355 in z_final's own dtype: float64 (F32 = false, z_final came
+// out of the SRC or the EQ) or float32 (F32 = true: SRC and EQ both bypassed,
+// z_final is the loader's float32 array).  nan_to_num maps NaN to 0 and +-inf
+// to +-(the dtype's max), so an infinite peak is that max too.
+template <bool F32>
 __global__ __launch_bounds__(kIoNT) void k_quantize16(const float* __restrict__ z, int64_t n,
                                                      int64_t ld_z, int16_t* __restrict__ out,
                                                      int64_t ld_out,
                                                      const uint32_t* __restrict__ peak) {
+  typedef typename std::conditional<F32, float, double>::type real;
+  const real big = F32 ? (real)FLT_MAX : (real)DBL_MAX;
   const int64_t b = blockIdx.y;
   const uint32_t pu = peak[b];
-  // nan_to_num maps +-inf to +-DBL_MAX, so an infinite peak is DBL_MAX.
-  const double pk = pu == 0x7f800000u ? DBL_MAX : (double)__uint_as_float(pu);
+  const real pk = pu == 0x7f800000u ? big : (real)__uint_as_float(pu);
   const float* r = z + b * ld_z;
   int16_t* o = out + b * ld_out;
   const int64_t stride = (int64_t)gridDim.x * kIoNT;
   for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < n; i += stride) {
-    double v = (double)r[i];
-    if (v != v) v = 0.0;
-    else if (v == INFINITY) v = DBL_MAX;
-    else if (v == -INFINITY) v = -DBL_MAX;
-    if (pk > 0.0) v /= pk;
-    o[i] = (int16_t)(int)(v * 32767.0);  // truncation toward zero, |v * 32767| <= 32767
+    real v = (real)r[i];
+    if (v != v) v = 0;
+    else if (v == (real)INFINITY) v = big;
+    else if (v == -(real)INFINITY) v = -big;
+    if (pk > 0) v /= pk;
+    o[i] = (int16_t)(int)(v * (real)32767);  // truncation toward zero, |v * 32767| <= 32767
   }
 }
 
@@ -280,15 +288,20 @@ int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double thr
 }
 
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
-                          int64_t ld_out, uint32_t* peak, hipStream_t s) {
+                          int64_t ld_out, uint32_t* peak, int precision, hipStream_t s) {
   DSP_REQUIRE(B >= 0 && n >= 0 && ld_z >= n && ld_out >= n, "bad sizes");
+  DSP_REQUIRE(precision == 32 || precision == 64, "precision %d is not 32 or 64", precision);
   if (B == 0) return DSP_OK;
   DSP_REQUIRE(z && out && peak, "null pointer");
   TraceScope trace("quantize16", s);
   if (int rc = absmax(z, B, n, ld_z, peak, true, s)) return rc;
   if (n == 0) return DSP_OK;
-  hipLaunchKernelGGL(k_quantize16, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z, n,
-                     ld_z, out, ld_out, peak);
+  if (precision == 32)
+    hipLaunchKernelGGL(k_quantize16<true>, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z,
+                       n, ld_z, out, ld_out, peak);
+  else
+    hipLaunchKernelGGL(k_quantize16<false>, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z,
+                       n, ld_z, out, ld_out, peak);
   DSP_LAUNCHED("k_quantize16");
   return DSP_OK;
 }

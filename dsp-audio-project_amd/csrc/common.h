@@ -104,7 +104,7 @@ int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t
 int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
                           uint32_t* peak, hipStream_t s);
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
-                          int64_t ld_out, uint32_t* peak, hipStream_t s);
+                          int64_t ld_out, uint32_t* peak, int precision, hipStream_t s);
 
 // Chain fast path: pass 1 of the fused cascade reads the SRC input xs through
 // the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).

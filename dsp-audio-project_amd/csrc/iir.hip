@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
   const int64_t b = blockIdx.x;
   const bool live = c < C;
   const int64_t t_begin = (int64_t)c * T;
-  // Pass-2 row descriptors (pass 1 of mode 2 reads other rows first).
+  // Pass-2 row descriptors (the x-state pass 1 reads other rows first).
   const int64_t in2 = live ? b * ld_x + t_begin : 0;
   const int len2 = live ? (int)min(T, n - t_begin) : 0;
   if constexpr (P1 == 2) {

@@ -75,7 +75,8 @@ _SIGNATURES = {
         _vp, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "dsp_peak_normalize_f32": (ctypes.c_int, [
         _vp, _c_i64, _c_i64, _c_i64, ctypes.c_double, _vp, _vp]),
-    "dsp_quantize_pcm16": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp]),
+    "dsp_quantize_pcm16": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _c_i32,
+                                          _vp]),
     "dsp_wav_header_pcm16": (ctypes.c_int, [ctypes.c_char_p, _c_i32, _c_i32, _c_i64]),
     "dsp_trace_enable": (ctypes.c_int, [_c_i32]),
     "dsp_trace_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _c_i32]),

@@ -136,8 +136,13 @@ def load_batch(sources, device: torch.device | str | None = None):
     return batch, [r[0].numel() for r in rows], [r[1] for r in rows]
 
 
-def quantize_pcm16(z: torch.Tensor) -> torch.Tensor:
-    """app.py:349-355 on the device: int16 [B, n] from float32 z [B, n]."""
+def quantize_pcm16(z: torch.Tensor, precision: int = 64) -> torch.Tensor:
+    """app.py:349-355 on the device: int16 [B, n] from float32 z [B, n].
+
+    precision: the dtype the app's z_final has, whose arithmetic the
+    quantiser reproduces -- 64 (float64: z_final came out of
+    conversion_tasa_muestreo or sistema_ecualizador) or 32 (float32: both were
+    bypassed and z_final is the loader's float32 array)."""
     squeeze = z.dim() == 1
     if squeeze:
         z = z.unsqueeze(0)
@@ -150,14 +155,15 @@ def quantize_pcm16(z: torch.Tensor) -> torch.Tensor:
     lib = _lib.load()
     with torch.cuda.device(z.device):
         rc = lib.dsp_quantize_pcm16(z.data_ptr(), out.data_ptr(), B, n, ops.ld(z), ops.ld(out),
-                                    peaks.data_ptr(), ops._stream(z.device))
+                                    peaks.data_ptr(), int(precision), ops._stream(z.device))
     _lib.check(rc, "dsp_quantize_pcm16")
     return out[0] if squeeze else out
 
 
-def wav_bytes_pcm16(z: torch.Tensor, fs: int) -> bytes:
-    """The WAV file app.py:352 writes for z (scipy.io.wavfile.write of int16)."""
-    pcm = quantize_pcm16(z if z.dim() == 1 else z[0]).cpu().numpy()
+def wav_bytes_pcm16(z: torch.Tensor, fs: int, precision: int = 64) -> bytes:
+    """The WAV file app.py:352 writes for z (scipy.io.wavfile.write of int16);
+    precision as in quantize_pcm16."""
+    pcm = quantize_pcm16(z if z.dim() == 1 else z[0], precision).cpu().numpy()
     header = ctypes.create_string_buffer(44)
     rc = _lib.load().dsp_wav_header_pcm16(header, int(fs), 1, pcm.size)
     _lib.check(rc, "dsp_wav_header_pcm16")

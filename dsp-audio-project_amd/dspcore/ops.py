@@ -9,6 +9,7 @@ FFT data), one row per audio channel.
 from __future__ import annotations
 
 import threading
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -18,7 +19,26 @@ from .design import SrcPlan, chunk_len_for, hann, max_chunks_for, state_response
 from .design import xstate_table as xstate_table_host
 
 _tables_lock = threading.Lock()
-_tables: dict = {}
+_tables: OrderedDict = OrderedDict()   # every device LUT kind, one LRU
+TABLE_CACHE_MAX = 256                  # entries (slider sweeps make new keys)
+
+
+def _cached(key, build):
+    """The device LUT for `key`, built by `build()` on a miss; one LRU of at
+    most TABLE_CACHE_MAX entries for every kind (hann, twiddles, Bluestein,
+    G, GX).  Callers that hold a table keep it alive past its eviction."""
+    with _tables_lock:
+        t = _tables.get(key)
+        if t is not None:
+            _tables.move_to_end(key)
+            return t
+    t = build()
+    with _tables_lock:
+        t = _tables.setdefault(key, t)
+        _tables.move_to_end(key)
+        while len(_tables) > TABLE_CACHE_MAX:
+            _tables.popitem(last=False)
+    return t
 
 
 def require_gpu() -> None:
@@ -39,19 +59,13 @@ def _ptr(t: torch.Tensor | None) -> int | None:
 
 def _table(kind: str, n: int, device: torch.device) -> torch.Tensor:
     """Cached per-device LUTs: Hann window (fp32[n]) and twiddles (fp32[2*(n/2)])."""
-    key = (kind, n, device.index)
-    t = _tables.get(key)
-    if t is None:
-        with _tables_lock:
-            t = _tables.get(key)
-            if t is None:
-                if kind == "hann":
-                    host = hann(n).astype(np.float32)
-                else:
-                    host = twiddles(n).astype(np.complex64).view(np.float32)
-                t = torch.from_numpy(np.ascontiguousarray(host)).to(device)
-                _tables[key] = t
-    return t
+    def build():
+        if kind == "hann":
+            host = hann(n).astype(np.float32)
+        else:
+            host = twiddles(n).astype(np.complex64).view(np.float32)
+        return torch.from_numpy(np.ascontiguousarray(host)).to(device)
+    return _cached((kind, n, device.index), build)
 
 
 def _rows(x: torch.Tensor, name: str) -> torch.Tensor:
@@ -108,18 +122,8 @@ def state_table(sos: np.ndarray, chunk_len: int, device: torch.device) -> torch.
     S = sos.shape[0]
     if S == 0 or S == 7 or S > 8:
         return None
-    key = ("G", sos.tobytes(), chunk_len, device.index)
-    t = _tables.get(key)
-    if t is None:
-        with _tables_lock:
-            t = _tables.get(key)
-            if t is None:
-                if len(_tables) > 256:  # bound the cache under slider sweeps
-                    for k in [k for k in _tables if k[0] == "G"]:
-                        del _tables[k]
-                t = torch.from_numpy(state_response_table(sos, chunk_len)).to(device)
-                _tables[key] = t
-    return t
+    return _cached(("G", sos.tobytes(), chunk_len, device.index),
+                   lambda: torch.from_numpy(state_response_table(sos, chunk_len)).to(device))
 
 
 def xstate_geometry(chunk_len: int, plan: SrcPlan) -> tuple[int, int, int]:
@@ -139,16 +143,8 @@ def xstate_table(sos: np.ndarray, plan: SrcPlan, chunk_len: int,
     """Cached device copy of design.xstate_table and its row count."""
     _, q0, rows = xstate_geometry(chunk_len, plan)
     key = ("GX", sos.tobytes(), plan.L, plan.M, plan.K, plan.c_offset, chunk_len, device.index)
-    t = _tables.get(key)
-    if t is None:
-        with _tables_lock:
-            t = _tables.get(key)
-            if t is None:
-                if len(_tables) > 256:
-                    for k in [k for k in _tables if k[0] in ("G", "GX")]:
-                        del _tables[k]
-                t = torch.from_numpy(xstate_table_host(sos, plan, chunk_len, q0, rows)).to(device)
-                _tables[key] = t
+    t = _cached(key, lambda: torch.from_numpy(
+        xstate_table_host(sos, plan, chunk_len, q0, rows)).to(device))
     return t, rows
 
 
@@ -179,20 +175,14 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
 
 
 def _dft_tables(n: int, device: torch.device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    key = ("BLU", n, device.index)
-    t = _tables.get(key)
-    if t is None:
-        with _tables_lock:
-            t = _tables.get(key)
-            if t is None:
-                from .design import bluestein_tables
-                chirp, bf, M = bluestein_tables(n)
-                if M != _lib.load().dsp_dft_size(n):
-                    raise RuntimeError("Bluestein size mismatch between host and library")
-                t = tuple(torch.from_numpy(a.astype(np.complex64).view(np.float32)).to(device)
-                          for a in (chirp, bf)) + (_table("tw", M, device),)
-                _tables[key] = t
-    return t
+    def build():
+        from .design import bluestein_tables
+        chirp, bf, M = bluestein_tables(n)
+        if M != _lib.load().dsp_dft_size(n):
+            raise RuntimeError("Bluestein size mismatch between host and library")
+        return tuple(torch.from_numpy(a.astype(np.complex64).view(np.float32)).to(device)
+                     for a in (chirp, bf)) + (_table("tw", M, device),)
+    return _cached(("BLU", n, device.index), build)
 
 
 def dft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -234,9 +234,13 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
  *                        peak_out: caller's device uint32[B], receives the
  *                        peaks as float32 bit patterns.
  * Playback, replacing app.py:349-355 (nan_to_num, divide by max|z| when > 0,
- * * 32767, astype(int16), all float64):
+ * * 32767, astype(int16), all in z_final's dtype):
  *   dsp_quantize_pcm16   DEVICE: float32 z [B][ld_z] -> int16 [B][ld_out],
- *                        peak_out as above (after nan_to_num);
+ *                        peak_out as above (after nan_to_num); `precision`
+ *                        64: the arithmetic in float64 (z_final came out of
+ *                        the SRC or the EQ, both return float64), 32: in
+ *                        float32 (SRC and EQ both bypassed: z_final is the
+ *                        loader's float32 array);
  *   dsp_wav_header_pcm16 HOST: the 44-byte header scipy.io.wavfile.write puts
  *                        in front of 16-bit PCM (app.py:352).
  * ------------------------------------------------------------------------- */
@@ -259,7 +263,7 @@ int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t c
 int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
                            uint32_t* peak_out, void* stream);
 int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
-                       int64_t ld_out, uint32_t* peak_out, void* stream);
+                       int64_t ld_out, uint32_t* peak_out, int32_t precision, void* stream);
 int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,
                          int64_t frames);
 

@@ -52,8 +52,10 @@ def load_audio(data):
 
 def playback_pcm16(z):
     """app.py:349-355: nan_to_num, divide by the peak when > 0, * 32767,
-    astype(int16), in float64."""
-    y = np.nan_to_num(np.asarray(z, dtype=np.float64))
+    astype(int16), in z's own dtype (float64 after the SRC or the EQ, the
+    loader's float32 when both are bypassed)."""
+    z = np.asarray(z)
+    y = np.nan_to_num(z.astype(z.dtype if z.dtype in (np.float32, np.float64) else np.float64))
     peak = np.max(np.abs(y))
     if peak > 0:
         y /= peak

@@ -88,18 +88,32 @@ def test_peak_normalize_nan_and_threshold(gpu):
 
 
 def test_playback_quantization_matches_app_bitwise(gpu):
+    """app.py:349-355 bitwise, in both dtypes z_final can have: float64 (after
+    the SRC or the EQ) and float32 (both bypassed: the loader's array).  The
+    data has samples where the two dtypes round to different int16 values, so
+    each mode is checked against its own restatement."""
     from dspcore import audio_io
     from oracle import dsp_ref_cpu as orc
     rng = np.random.default_rng(8)
-    z = rng.uniform(-1, 1, (4, 5000)).astype(np.float32)
+    z = rng.uniform(-1, 1, (4, 200000)).astype(np.float32)
     z[1, 10] = np.nan
     z[2, :] = 0.0
     z[3, 7] = np.inf
     z[3, 8] = -np.inf
-    q = audio_io.quantize_pcm16(torch.from_numpy(z).to(gpu)).cpu().numpy()
+    zt = torch.from_numpy(z).to(gpu)
+    q64 = audio_io.quantize_pcm16(zt).cpu().numpy()
+    q32 = audio_io.quantize_pcm16(zt, precision=32).cpu().numpy()
+    differ = 0
     for b in range(4):
-        np.testing.assert_array_equal(q[b], orc.playback_pcm16(z[b]))
+        r64 = orc.playback_pcm16(z[b].astype(np.float64))
+        r32 = orc.playback_pcm16(z[b])
+        np.testing.assert_array_equal(q64[b], r64)
+        np.testing.assert_array_equal(q32[b], r32)
+        differ += int(np.count_nonzero(r64 != r32))
+    assert differ > 0          # the two modes are distinguishable on this data
     wav = audio_io.wav_bytes_pcm16(torch.from_numpy(z[0]).to(gpu), 72000)
     buf = io.BytesIO()
-    wavfile.write(buf, 72000, orc.playback_pcm16(z[0]))
+    wavfile.write(buf, 72000, orc.playback_pcm16(z[0].astype(np.float64)))
     assert wav == buf.getvalue()
+    with pytest.raises(ValueError):
+        audio_io.quantize_pcm16(zt, precision=16)

@@ -492,3 +492,67 @@ def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
                                        None, 4096)
         assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL
         assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+
+
+def test_chain_config4_one_gpu_and_shards(gpu):
+    """Config 4 on one GPU (32768 x 48000: 2.36e9 output elements, row offsets
+    past 2^31): spot rows against the oracle, including row 32767, and the
+    last shard of the 2-, 4- and 8-GPU splits (16384 / 8192 / 4096 channels,
+    bench.py's per-rank batches) bitwise equal to the full run's rows."""
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.shard import shard_ranges
+    from oracle import dsp_ref_cpu as orc
+    B = 32768
+    cfg = ChainConfig(48000, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len > 0
+    gen = torch.Generator(device=gpu).manual_seed(4)
+    x = torch.rand((B, 48000), generator=gen, device=gpu) * 2 - 1
+    y, z, mag = ch.run(x)
+    torch.cuda.synchronize()
+    assert ch.handoff_ok()
+    assert float(z.abs().max()) <= 1.0 and torch.isfinite(mag).all()
+    for b in (0, 16383, 16384, 32767):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, orc.CONFIG3_GAINS,
+                                       None, 4096)
+        assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL
+        assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+    for parts in (2, 4, 8):
+        lo, hi = shard_ranges(B, parts)[-1]
+        sh = Chain(cfg, hi - lo, gpu, plan_batch=B)
+        ys, zs, ms = sh.run(x[lo:hi])
+        assert torch.equal(ys, y[lo:hi]) and torch.equal(zs, z[lo:hi]) and torch.equal(ms, mag[lo:hi])
+        assert sh.handoff_ok()
+        del sh, ys, zs, ms
+
+
+def test_shards_plan_with_the_job_batch(gpu):
+    """Two-launch geometry (config 5's L/M = 160/147), 4096 rows: planned with
+    the job's batch (Chain(plan_batch=4096)) every shard of 1, 2 and 4 runs the
+    unsharded chunking and the rows are bitwise equal although the per-shard
+    batches (2048, 1024) straddle design.WIDE_BATCH; planned per shard they
+    agree to float64 rounding."""
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.shard import run_sharded
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 4096, 4800
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-1, 1, (B, n_in)).astype(np.float32)
+    cfg = ChainConfig(n_in, 44100, 160, 147, 1023, orc.CONFIG3_GAINS, n_fft=2048)
+
+    def fn(plan):
+        def run(xd):
+            ch = Chain(cfg, xd.shape[0], xd.device, plan_batch=plan)
+            assert ch.tile_len == 0
+            y, z, mag = ch.run(xd)
+            return z.clone(), mag.clone()
+        return run
+
+    base = run_sharded(fn(B), x, [gpu])
+    for parts in (2, 4):
+        got = run_sharded(fn(B), x, [gpu] * parts)
+        for a, b in zip(got, base):
+            np.testing.assert_array_equal(a, b)
+    own = run_sharded(fn(None), x, [gpu] * 4)
+    assert np.max(np.abs(own[0] - base[0])) <= 2e-6

@@ -1,15 +1,22 @@
+# GPU parity tests, smoke and bench lines -> gpurun_out/$TAG/.
+#   bash tools/gpu_check.sh TAG [bench configs...]   (default: c4; "none" skips)
 set -o pipefail
+TAG=${1:-check}
+shift
+CFGS=${*:-c4}
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-echo "== pytest gpu" 
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -30 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+OUT="$GRAFT_REPO_ROOT/gpurun_out/$TAG"
+rm -rf "$OUT"; mkdir -p "$OUT"
+echo "== pytest gpu"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; grep -E "PASSED|FAILED|ERROR" "$OUT/pytest_gpu.log" | tail -3; tail -3 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
 echo "== smoke"
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -3 || exit 1
-echo "== bench"
-timeout -k 10 600 python bench.py > gpurun_out/bench_r01.json 2> gpurun_out/bench_r01.err || { tail -20 gpurun_out/bench_r01.err; exit 1; }
-cat gpurun_out/bench_r01.json
-echo "== rocprof"
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_r01" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --cpu-sample 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_r01.log" 2>&1 || { tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof_r01.log"; exit 1; }
-find "$GRAFT_REPO_ROOT/gpurun_out/prof_r01" -name "*stats*" | head
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+for c in $CFGS; do
+  [ "$c" = none ] && continue
+  echo "== bench $c"
+  timeout -k 10 600 python bench.py --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
+  cut -c1-400 "$OUT/bench_$c.json"
+  python -c "import json,sys; d=json.load(open('$OUT/bench_$c.json')); print('value', d['value'], 'ms', d['ms_per_step'], 'kernels', d['kernels_ms'], 'frac', d['roofline']['frac'], 'chain', d['chain_roofline']['frac'], 'cfg3', (d.get('config3') or {}).get('ms_per_step'), (d.get('config3') or {}).get('kernels_ms'), 'cpu', (d.get('cpu_baseline') or {}).get('value'), (d.get('cpu_baseline') or {}).get('cores'))"
+done

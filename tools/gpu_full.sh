@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { t
 cat "$OUT/bench.json"
 echo "== rocprof stats"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --cpu-sample 0 > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --cpu-per-proc 0 --no-config3 --config c3 > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 cat "$OUT/kernel_stats.csv" | cut -d, -f1-8 | head -12
 echo "== pmc"
