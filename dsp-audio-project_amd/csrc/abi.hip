@@ -90,12 +90,17 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
                             static_cast<hipStream_t>(stream));
 }
 
+size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n) {
+  return dsp::fft_workspace_bytes(B, log2n);
+}
+
 int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
-                       const float* twiddles, void* stream) {
+                       const float* twiddles, void* workspace, size_t workspace_bytes,
+                       void* stream) {
   dsp::clear_error();
-  return dsp::launch_fft(in, out, B, log2n, real_input, ld_in, ld_out, twiddles,
-                         static_cast<hipStream_t>(stream));
+  return dsp::launch_fft(in, out, B, log2n, real_input, ld_in, ld_out, twiddles, workspace,
+                         workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 int dsp_dft_size(int64_t n) {
@@ -116,10 +121,12 @@ int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_
 int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                      int64_t seg_start, int64_t seg_len, int32_t log2n,
                      int64_t ld_mag, const float* window,
-                     const float* twiddles, void* stream) {
+                     const float* twiddles, void* workspace, size_t workspace_bytes,
+                     void* stream) {
   dsp::clear_error();
   return dsp::launch_spectrum(x, mag, B, ld_x, seg_start, seg_len, log2n, ld_mag,
-                              window, twiddles, static_cast<hipStream_t>(stream));
+                              window, twiddles, workspace, workspace_bytes,
+                              static_cast<hipStream_t>(stream));
 }
 
 int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
@@ -180,6 +187,9 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   dsp::clear_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
+  if (log2n < 0 || log2n > DSP_MAX_LOG2N)
+    return dsp::set_error(DSP_EINVAL, "chain spectrum log2n=%d outside [0, %d]", log2n,
+                          DSP_MAX_LOG2N);
   if (B == 0) return DSP_OK;
   int rc = dsp::kNotFused;
   if (dsp::g_chain_path == 0)
@@ -200,7 +210,7 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   }
   if (rc) return rc;
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
-                              twiddles, s);
+                              twiddles, nullptr, 0, s);
 }
 
 int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info) {

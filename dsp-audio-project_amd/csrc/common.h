@@ -84,7 +84,7 @@ int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
 int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,
-                    hipStream_t s);
+                    void* ws, size_t ws_bytes, hipStream_t s);
 int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
                 int64_t seg_len, int64_t hop, int64_t frames, int log2n, int64_t ld_mag,
                 const float* window, const float* tw, hipStream_t s);
@@ -93,7 +93,9 @@ int launch_dft(const float* in, float* out, int64_t B, int64_t n, int real_in, i
                int64_t ld_out, const float* chirp, const float* chirp_fft, const float* tw_m,
                hipStream_t s);
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
-               int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s);
+               int64_t ld_in, int64_t ld_out, const float* tw, void* ws, size_t ws_bytes,
+               hipStream_t s);
+size_t fft_workspace_bytes(int64_t B, int log2n);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 
 // Audio I/O (audio_io.hip).

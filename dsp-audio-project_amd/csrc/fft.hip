@@ -208,10 +208,11 @@ struct Tw {
 template <int LOG2N>
 struct Tw<LOG2N, 15> {};
 
-// TSTR: stride into the caller's table (2 when the table is for 2N points).
-template <int LOG2N, int P, int TSTR = 1>
+// tstr: stride into the caller's table (2 when the table is for 2N points,
+// N_total / N for a sub-transform of a four-step FFT).
+template <int LOG2N, int P>
 __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restrict__ table,
-                                        int j0) {
+                                        int j0, int64_t tstr = 1) {
   using PL = Plan<LOG2N>;
   if constexpr (P + 1 < PL::NP) {
     constexpr int R = PL::radix(P + 1);
@@ -219,9 +220,9 @@ __device__ __forceinline__ void load_tw(Tw<LOG2N, P>& tw, const float2* __restri
 #pragma unroll
     for (int b = 0; b < PL::RMAX / R; ++b) {
       const int m = (j0 + b * PL::TPT) & (NS - 1);
-      tw.w[b] = table[m * (PL::N / (NS * R)) * TSTR];
+      tw.w[b] = table[(int64_t)m * (PL::N / (NS * R)) * tstr];
     }
-    load_tw<LOG2N, P + 1, TSTR>(tw.next, table, j0);
+    load_tw<LOG2N, P + 1>(tw.next, table, j0, tstr);
   }
 }
 
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(Plan<LOG2N - 1>::NT) void k_spec_real(FftArgs a) {
   const bool live = t < a.B;
   float2* buf = lds + tl * PL::PADN;
   Tw<LOG2N - 1, 0> tw;
-  load_tw<LOG2N - 1, 0, 2>(tw, a.tw, j0);
+  load_tw<LOG2N - 1, 0>(tw, a.tw, j0, 2);
   run_pass<LOG2N - 1, 0>(RealSpecIO<NH>{a, in_row<kSpec>(a, live ? t : 0), buf, live}, buf, j0,
                          tw);
   __syncthreads();  // the last pass stored Z into LDS
@@ -375,6 +376,136 @@ int launch_spec_real(const FftArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_spec_real<LOG2N>, dim3(grid), dim3(PL::NT), shm, s, a);
   DSP_LAUNCHED("k_spec_real");
   return DSP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Four-step FFT for N = 2^15 .. 2^DSP_MAX_LOG2N_FFT (beyond one workgroup's
+// LDS): N = NA * NB, n = n1 + NB n2, k = k2 + NA k1 (n1, k1 < NB; n2, k2 < NA)
+//   step A: Y[n1][k2] = W_N^(n1 k2) * sum_n2 x[n1 + NB n2] W_NA^(n2 k2)
+//           -> workspace[k2][n1]
+//   step B: X[k2 + NA k1] = sum_n1 Y[n1][k2] W_NB^(n1 k1)
+// Each workgroup runs kCols sub-transforms of consecutive columns (step A) or
+// rows (step B) in LDS with the one-launch Stockham passes; the HBM side of
+// both steps moves kCols consecutive complex values (64 B) per index, staged
+// through LDS so every global access is a run of consecutive addresses.  The
+// sub-transforms' twiddles come from the caller's W_N table at stride N/NA
+// (N/NB), the inter-step twiddle W_N^m from the same table (m < N/2, else its
+// negation).  The workspace holds Y: B x N complex.
+// ---------------------------------------------------------------------------
+constexpr int kCols = 8;
+
+template <int N>
+struct LdsIO {
+  static constexpr bool kLdsIn = true;
+  float2* buf;
+  __device__ __forceinline__ float2 load(int n) const { return buf[lpad(n)]; }
+  __device__ __forceinline__ void store(int k, float2 v) const { buf[lpad(k)] = v; }
+};
+
+__device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
+  m &= N - 1;
+  const float2 w = tw[m < N / 2 ? m : m - N / 2];
+  return m < N / 2 ? w : make_float2(-w.x, -w.y);
+}
+
+struct Fft4Args {
+  FftArgs a;          // in / out / rows / segment / window / W_N table
+  float2* ws;         // B x N complex
+  int64_t N;          // NA * NB
+};
+
+template <int LOG2A, int MODE>
+__global__ __launch_bounds__(kCols * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
+  using PL = Plan<LOG2A>;
+  constexpr int NA = PL::N, NT = kCols * PL::TPT, TS = PL::PADN + 1;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const FftArgs& a = f.a;
+  const int64_t NB = f.N / NA;
+  const int64_t b = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * kCols;
+  const InRow ir = in_row<MODE>(a, b);
+  for (int i = threadIdx.x; i < kCols * NA; i += NT) {
+    const int c = i % kCols, n2 = i / kCols;
+    lds[c * TS + lpad(n2)] = load_input<MODE>(a, ir, (int)(c0 + c + NB * n2), true);
+  }
+  const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
+  Tw<LOG2A, 0> tw;
+  load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA);
+  __syncthreads();
+  run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
+  __syncthreads();
+  float2* y = f.ws + b * f.N;
+  for (int i = threadIdx.x; i < kCols * NA; i += NT) {
+    const int c = i % kCols, k2 = i / kCols;
+    const int64_t n1 = c0 + c;
+    y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], tw_full(a.tw, n1 * k2, f.N));
+  }
+}
+
+template <int LOG2B, int MODE>
+__global__ __launch_bounds__(kCols * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
+  using PL = Plan<LOG2B>;
+  constexpr int NB = PL::N, NT = kCols * PL::TPT, TS = PL::PADN + 1;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const FftArgs& a = f.a;
+  const int64_t NA = f.N / NB;
+  const int64_t b = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * kCols;  // first k2 row
+  const float2* y = f.ws + b * f.N;
+  for (int i = threadIdx.x; i < kCols * NB; i += NT) {
+    const int r = i / NB, n1 = i - r * NB;
+    lds[r * TS + lpad(n1)] = y[(r0 + r) * NB + n1];
+  }
+  const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
+  Tw<LOG2B, 0> tw;
+  load_tw<LOG2B, 0>(tw, a.tw, j0, f.N / NB);
+  __syncthreads();
+  run_pass<LOG2B, 0>(LdsIO<NB>{lds + tl * TS}, lds + tl * TS, j0, tw);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kCols * NB; i += NT) {
+    const int c = i % kCols, k1 = i / kCols;
+    const int64_t k = r0 + c + NA * k1;
+    const float2 v = lds[c * TS + lpad(k1)];
+    if constexpr (MODE == kSpec) {
+      if (k <= f.N / 2) a.out[b * a.ld_out + k] = sqrtf(fmaf(v.x, v.x, v.y * v.y));
+    } else {
+      reinterpret_cast<float2*>(a.out)[b * a.ld_out + k] = v;
+    }
+  }
+}
+
+template <int LOG2A, int LOG2B, int MODE>
+int launch_fft4(const Fft4Args& f, hipStream_t s) {
+  using PA = Plan<LOG2A>;
+  using PB = Plan<LOG2B>;
+  static_assert(LOG2A >= 4 && LOG2B >= LOG2A, "split");
+  const size_t sa = (size_t)kCols * (PA::PADN + 1) * sizeof(float2);
+  const size_t sb = (size_t)kCols * (PB::PADN + 1) * sizeof(float2);
+  if (int rc = allow_lds(k_fft4_a<LOG2A, MODE>, sa)) return rc;
+  if (int rc = allow_lds(k_fft4_b<LOG2B, MODE>, sb)) return rc;
+  const unsigned rows = (unsigned)f.a.B;
+  hipLaunchKernelGGL((k_fft4_a<LOG2A, MODE>), dim3((unsigned)(PB::N / kCols), rows),
+                     dim3(kCols * PA::TPT), sa, s, f);
+  DSP_LAUNCHED("k_fft4_a");
+  hipLaunchKernelGGL((k_fft4_b<LOG2B, MODE>), dim3((unsigned)(PA::N / kCols), rows),
+                     dim3(kCols * PB::TPT), sb, s, f);
+  DSP_LAUNCHED("k_fft4_b");
+  return DSP_OK;
+}
+
+template <int MODE>
+int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
+  switch (log2n) {
+    case 15: return launch_fft4<7, 8, MODE>(f, s);
+    case 16: return launch_fft4<8, 8, MODE>(f, s);
+    case 17: return launch_fft4<8, 9, MODE>(f, s);
+    case 18: return launch_fft4<9, 9, MODE>(f, s);
+    case 19: return launch_fft4<9, 10, MODE>(f, s);
+    case 20: return launch_fft4<10, 10, MODE>(f, s);
+    case 21: return launch_fft4<10, 11, MODE>(f, s);
+    case 22: return launch_fft4<11, 11, MODE>(f, s);
+    default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
+  }
 }
 
 template <int MODE>
@@ -513,10 +644,54 @@ int dispatch(const FftArgs& a, int log2n, hipStream_t s) {
 
 }  // namespace
 
+size_t fft_workspace_bytes(int64_t B, int log2n) {
+  if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
+  return (size_t)B * ((size_t)1 << log2n) * sizeof(float2);
+}
+
+namespace {
+constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
+
+// Four-step transform of B rows, in launches of <= kMaxRows4 rows.
+template <int MODE>
+int run_fft4(FftArgs a, int log2n, void* ws, size_t ws_bytes, hipStream_t s) {
+  DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
+  const size_t need = fft_workspace_bytes(a.B, log2n);
+  DSP_REQUIRE(ws && ws_bytes >= need, "FFT workspace too small: %zu < %zu bytes", ws_bytes, need);
+  DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 7) == 0, "FFT workspace not 8-byte aligned");
+  const int64_t B = a.B;
+  for (int64_t b0 = 0; b0 < B; b0 += kMaxRows4) {
+    FftArgs part = a;
+    part.B = B - b0 < kMaxRows4 ? B - b0 : kMaxRows4;
+    part.in = a.in + b0 * a.ld_in * (MODE == kC2C ? 2 : 1);
+    part.out = a.out + b0 * a.ld_out * (MODE == kSpec ? 1 : 2);
+    const Fft4Args f{part, static_cast<float2*>(ws), int64_t(1) << log2n};
+    if (int rc = dispatch4<MODE>(f, log2n, s)) return rc;
+  }
+  return DSP_OK;
+}
+}  // namespace
+
 int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,
-                    hipStream_t s) {
+                    void* ws, size_t ws_bytes, hipStream_t s) {
+  if (log2n > DSP_MAX_LOG2N) {
+    DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n,
+                DSP_MAX_LOG2N_FFT);
+    const int64_t N = int64_t(1) << log2n;
+    DSP_REQUIRE(B >= 0 && seg_start >= 0 && seg_len >= 0 && seg_len <= N,
+                "bad segment start=%lld len=%lld (N=%lld)", (long long)seg_start,
+                (long long)seg_len, (long long)N);
+    DSP_REQUIRE(ld_mag >= N / 2 + 1, "ld_mag too small");
+    DSP_REQUIRE(ld_x >= seg_start + seg_len, "segment exceeds the row");
+    if (B == 0) return DSP_OK;
+    DSP_REQUIRE(x && mag && window && tw, "null pointer");
+    FftArgs a{x, mag, B, ld_x, ld_mag, seg_start, seg_len, 0, 1, window,
+              reinterpret_cast<const float2*>(tw)};
+    TraceScope trace("spectrum", s);
+    return run_fft4<kSpec>(a, log2n, ws, ws_bytes, s);
+  }
   return launch_stft(x, mag, B, ld_x, seg_start, seg_len, 0, 1, log2n, ld_mag, window, tw, s);
 }
 
@@ -543,9 +718,10 @@ int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg
 }
 
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
-               int64_t ld_in, int64_t ld_out, const float* tw, hipStream_t s) {
-  DSP_REQUIRE(log2n >= 0 && log2n <= DSP_MAX_LOG2N, "log2n=%d outside [0, %d]", log2n,
-              DSP_MAX_LOG2N);
+               int64_t ld_in, int64_t ld_out, const float* tw, void* ws, size_t ws_bytes,
+               hipStream_t s) {
+  DSP_REQUIRE(log2n >= 0 && log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n,
+              DSP_MAX_LOG2N_FFT);
   const int64_t N = int64_t(1) << log2n;
   DSP_REQUIRE(B >= 0 && ld_in >= N && ld_out >= N, "bad sizes");
   if (B == 0) return DSP_OK;
@@ -555,6 +731,9 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
               "complex buffers must be 8-byte aligned");
   FftArgs a{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, reinterpret_cast<const float2*>(tw)};
   TraceScope trace("fft", s);
+  if (log2n > DSP_MAX_LOG2N)
+    return real_in ? run_fft4<kR2C>(a, log2n, ws, ws_bytes, s)
+                   : run_fft4<kC2C>(a, log2n, ws, ws_bytes, s);
   return real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s);
 }
 

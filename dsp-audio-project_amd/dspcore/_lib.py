@@ -29,6 +29,7 @@ DSP_EHIP = -2
 DSP_ENOTSUP = -3
 DSP_MAX_STAGES = 16
 DSP_MAX_LOG2N = 14
+DSP_MAX_LOG2N_FFT = 22
 DSP_MAX_DFT = 8192
 
 _c_i32, _c_i64, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
@@ -45,11 +46,12 @@ _SIGNATURES = {
     "dsp_biquad_cascade_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _dp, _c_i32, _c_i32, _c_i64,
         _vp, _vp, _c_sz, _vp]),
+    "dsp_fft_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
     "dsp_fft_r2_c2c_f32": (ctypes.c_int, [
-        _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp]),
+        _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "dsp_spectrum_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp,
-        _vp]),
+        _vp, _c_sz, _vp]),
     "dsp_dft_size": (ctypes.c_int, [_c_i64]),
     "dsp_dft_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i32, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),

@@ -208,13 +208,22 @@ def dft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     return out
 
 
-def _log2(n: int) -> int:
+def _log2(n: int, limit: int | None = None) -> int:
+    """log2 of a power-of-two length; `limit` defaults to the largest FFT
+    (DSP_MAX_LOG2N_FFT; the STFT stays within one LDS-resident launch)."""
     if n < 1 or n & (n - 1):
         raise ValueError(f"length {n} is not a power of two; the radix-2 FFT needs 2^k points")
     lg = n.bit_length() - 1
-    if lg > _lib.DSP_MAX_LOG2N:
-        raise RuntimeError(f"FFT length 2^{lg} exceeds the LDS-resident limit 2^{_lib.DSP_MAX_LOG2N}")
+    limit = _lib.DSP_MAX_LOG2N_FFT if limit is None else limit
+    if lg > limit:
+        raise RuntimeError(f"FFT length 2^{lg} exceeds the supported 2^{limit}")
     return lg
+
+
+def _fft_workspace(B: int, lg: int, device: torch.device) -> torch.Tensor | None:
+    """Scratch of the four-step transform above DSP_MAX_LOG2N (else None)."""
+    nbytes = int(_lib.load().dsp_fft_workspace_bytes(B, lg))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes else None
 
 
 def fft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -230,10 +239,12 @@ def fft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     if out is None:
         out = torch.empty((B, n), dtype=torch.complex64, device=x.device)
     tw = _table("tw", n, x.device)
+    ws = _fft_workspace(B, lg, x.device)
     lib = _lib.load()
     with torch.cuda.device(x.device):
         rc = lib.dsp_fft_r2_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), ld(x),
-                                    ld(out), _ptr(tw), _stream(x.device))
+                                    ld(out), _ptr(tw), _ptr(ws), 0 if ws is None else ws.numel(),
+                                    _stream(x.device))
     _lib.check(rc, "dsp_fft_r2_c2c_f32")
     return out
 
@@ -250,10 +261,12 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
         out = torch.empty((B, n_fft // 2 + 1), dtype=torch.float32, device=x.device)
     win = _table("hann", n_fft, x.device)
     tw = _table("tw", n_fft, x.device)
+    ws = _fft_workspace(B, lg, x.device)
     lib = _lib.load()
     with torch.cuda.device(x.device):
         rc = lib.dsp_spectrum_f32(_ptr(x), _ptr(out), B, ld(x), seg_start, seg_len,
-                                  lg, ld(out), _ptr(win), _ptr(tw), _stream(x.device))
+                                  lg, ld(out), _ptr(win), _ptr(tw), _ptr(ws),
+                                  0 if ws is None else ws.numel(), _stream(x.device))
     _lib.check(rc, "dsp_spectrum_f32")
     return out
 
@@ -266,7 +279,7 @@ def stft_magnitude(x: torch.Tensor, n_fft: int, hop: int, frames: int,
     if x.dtype != torch.float32:
         x = x.float()
     B, n = x.shape
-    lg = _log2(n_fft)
+    lg = _log2(n_fft, _lib.DSP_MAX_LOG2N)
     half = n_fft // 2 + 1
     if out is None:
         out = torch.empty((B, frames, half), dtype=torch.float32, device=x.device)

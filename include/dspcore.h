@@ -37,6 +37,7 @@ extern "C" {
 
 #define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
+#define DSP_MAX_LOG2N_FFT 22 /* largest FFT / spectrum (four-step above 2^14)  */
 #define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
 
 /* ABI version (major*10000 + minor*100 + patch). */
@@ -90,14 +91,20 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
 /* ---------------------------------------------------------------------------
  * Radix-2 decimation-in-time FFT, batched, natural-order output.
  * Replaces dsp_core.py:41-66 (fft_diezmado_en_tiempo).  N = 2^log2n,
- * 0 <= log2n <= DSP_MAX_LOG2N.  real_input != 0: `in` is float32 [B][ld_in]
- * real samples; otherwise interleaved complex [B][ld_in] (ld in complex
- * elements).  `out` is interleaved complex [B][ld_out].  `twiddles` is the
- * interleaved complex table exp(-2*pi*i*k/N), k < N/2, in float32.
+ * 0 <= log2n <= DSP_MAX_LOG2N_FFT.  real_input != 0: `in` is float32
+ * [B][ld_in] real samples; otherwise interleaved complex [B][ld_in] (ld in
+ * complex elements).  `out` is interleaved complex [B][ld_out].  `twiddles` is
+ * the interleaved complex table exp(-2*pi*i*k/N), k < N/2, in float32.
+ * Up to DSP_MAX_LOG2N one launch keeps each transform in LDS and needs no
+ * workspace; above it a four-step transform (two launches) keeps its
+ * intermediate in `workspace` (device, 8-byte aligned,
+ * >= dsp_fft_workspace_bytes(B, log2n) = B * N * 8 bytes; 0 below).
  * ------------------------------------------------------------------------- */
+size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n);
 int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
-                       const float* twiddles, void* stream);
+                       const float* twiddles, void* workspace, size_t workspace_bytes,
+                       void* stream);
 
 /* ---------------------------------------------------------------------------
  * Any-length DFT, batched (app.py:322-324 calls
@@ -121,12 +128,14 @@ int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_
  * Replaces dsp_core.py:74-98 (calcular_espectro_magnitud): segment
  * x[seg_start : seg_start + seg_len] zero-padded to N = 2^log2n (:76-82),
  * times window[N] (Hann, :85-87), FFT (:90), |X[k]| for k <= N/2 (:91,:97-98).
- * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.
+ * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.  log2n <= DSP_MAX_LOG2N_FFT;
+ * above DSP_MAX_LOG2N the workspace rules of dsp_fft_r2_c2c_f32 apply.
  * ------------------------------------------------------------------------- */
 int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                      int64_t seg_start, int64_t seg_len, int32_t log2n,
                      int64_t ld_mag, const float* window,
-                     const float* twiddles, void* stream);
+                     const float* twiddles, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------
  * Framed magnitude spectrogram (every frame instead of

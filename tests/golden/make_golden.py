@@ -183,6 +183,30 @@ def main(root="/root/reference"):
                       f"{tag}_f": f, f"{tag}_mag2048": m2, f"{tag}_fs_out": np.array(fs_out)})
     np.savez_compressed(os.path.join(HERE, "chain.npz"), **chain)
 
+    # (9) FFT above the one-launch size, N = 2^13 .. 2^16: real rows for every
+    # size, complex rows for 2^15 and 2^16, plus the spectrum recipe at
+    # n_fft = 2^15 on a 100000-sample signal.  Own seed (the fixtures above
+    # stay as they were); inputs stored as float32 / complex64 (exactly what
+    # the reference was given), outputs rounded to complex64 / float32
+    # (6e-8 relative, far inside the 1e-5 tolerance) to keep the file small.
+    rng9 = np.random.default_rng(20261016)
+    big = {}
+    for k in (13, 14, 15, 16):
+        n = 1 << k
+        xr = rng9.uniform(-1, 1, n).astype(np.float32)
+        big[f"xr_{k}"] = xr
+        big[f"Xr_{k}"] = np.asarray(ref.fft_diezmado_en_tiempo(xr.astype(np.float64)),
+                                    dtype=np.complex128).astype(np.complex64)
+        if k >= 15:
+            xc = (rng9.uniform(-1, 1, n) + 1j * rng9.uniform(-1, 1, n)).astype(np.complex64)
+            big[f"xc_{k}"] = xc
+            big[f"Xc_{k}"] = np.asarray(ref.fft_diezmado_en_tiempo(xc.astype(np.complex128)),
+                                        dtype=np.complex128).astype(np.complex64)
+    zs = noise(rng9, (100000,))
+    fs15, ms15 = spectrum_via_primitives(ref, zs.astype(np.float64), 72000, 1 << 15)
+    big["spec_x"], big["spec_f"], big["spec_m"] = zs, fs15, ms15.astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "fft_large.npz"), **big)
+
     manifest = {"numpy": np.__version__, "scipy": scipy.__version__,
                 "reference": "Renatovela-ctrl/dsp-audio-project modules/dsp_core.py",
                 "generator": "tests/golden/make_golden.py", "seed": 20261015}

@@ -556,3 +556,56 @@ def test_shards_plan_with_the_job_batch(gpu):
             np.testing.assert_array_equal(a, b)
     own = run_sharded(fn(None), x, [gpu] * 4)
     assert np.max(np.abs(own[0] - base[0])) <= 2e-6
+
+
+def test_fft_four_step_matches_reference(gpu):
+    """N = 2^13 .. 2^16 through the drop-in against the reference's own outputs
+    (tests/golden/fft_large.npz; 2^15 and 2^16 take the four-step path), and
+    2^17 .. 2^22 batched against np.fft.fft: max|dX| <= 1e-5 * max|X|."""
+    dc = _dc()
+    g = golden("fft_large")
+    for k in (13, 14, 15, 16):
+        for kind in (("r", "c") if k >= 15 else ("r",)):
+            x = g[f"x{kind}_{k}"].astype(np.complex128 if kind == "c" else np.float64)
+            ref = g[f"X{kind}_{k}"].astype(np.complex128)
+            X = dc.fft_diezmado_en_tiempo(x)
+            assert X.dtype == np.complex128 and X.shape == ref.shape
+            err = np.max(np.abs(X - ref))
+            assert err <= FFT_RTOL * np.max(np.abs(ref)), f"N=2^{k} {kind}: {err:.3g}"
+    rng = np.random.default_rng(12)
+    for lg, B in ((17, 3), (18, 2), (19, 2), (20, 2), (21, 1), (22, 1)):
+        x = (rng.uniform(-1, 1, (B, 1 << lg)) + 1j * rng.uniform(-1, 1, (B, 1 << lg)))
+        x = x.astype(np.complex64)
+        X = _ops().fft(torch.from_numpy(x).to(gpu)).cpu().numpy()
+        ref = np.fft.fft(x.astype(np.complex128), axis=1)
+        err = np.max(np.abs(X - ref), axis=1)
+        assert np.all(err <= FFT_RTOL * np.max(np.abs(ref), axis=1)), (lg, err)
+    xr = rng.uniform(-1, 1, (2, 1 << 20)).astype(np.float32)
+    X = _ops().fft(torch.from_numpy(xr).to(gpu)).cpu().numpy()
+    ref = np.fft.fft(xr.astype(np.float64), axis=1)
+    assert np.max(np.abs(X - ref)) <= FFT_RTOL * np.max(np.abs(ref))
+    with pytest.raises(RuntimeError):
+        _ops().fft(torch.zeros((1, 1 << 23), device=gpu))
+
+
+def test_spectrum_four_step_matches_reference(gpu):
+    """calcular_espectro_magnitud with n_fft = 2^15 (four-step spectrum mode:
+    centre segment, Hann window, |X[k]| for k <= N/2) against the reference
+    recipe's output in tests/golden/fft_large.npz."""
+    dc = _dc()
+    g = golden("fft_large")
+    f, m = dc.calcular_espectro_magnitud(g["spec_x"].astype(np.float64), 72000, n_fft=1 << 15)
+    np.testing.assert_array_equal(f, g["spec_f"])
+    ref = g["spec_m"].astype(np.float64)
+    assert m.shape == ref.shape
+    assert np.max(np.abs(m - ref)) <= FFT_RTOL * np.max(ref)
+    # batched device rows against numpy at 2^18 (segment shorter than N: zero padded)
+    rng = np.random.default_rng(13)
+    x = rng.uniform(-1, 1, (2, 200000)).astype(np.float32)
+    mag = _ops().spectrum(torch.from_numpy(x).to(gpu), 1000, 150000, 1 << 18).cpu().numpy()
+    n = 1 << 18
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n) / (n - 1))
+    seg = np.zeros((2, n))
+    seg[:, :150000] = x[:, 1000:151000]
+    ref = np.abs(np.fft.fft(seg * w, axis=1))[:, :n // 2 + 1]
+    assert np.max(np.abs(mag - ref)) <= FFT_RTOL * np.max(ref)

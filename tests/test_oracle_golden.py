@@ -69,6 +69,22 @@ def test_fft_exact():
             np.testing.assert_array_equal(orc.fft_dit(g[f"x{kind}_{k}"]), g[f"X{kind}_{k}"])
 
 
+def test_fft_large_matches_reference():
+    """N = 2^13 .. 2^16 (fixtures stored as complex64): the restatement equals
+    the reference's outputs to the fixture's rounding."""
+    g = golden("fft_large")
+    for k in (13, 14, 15, 16):
+        kinds = ("r", "c") if k >= 15 else ("r",)
+        for kind in kinds:
+            x = g[f"x{kind}_{k}"].astype(np.complex128 if kind == "c" else np.float64)
+            ref = g[f"X{kind}_{k}"]
+            got = orc.fft_dit(x)
+            assert np.max(np.abs(got - ref)) <= 1e-6 * np.max(np.abs(ref)), (k, kind)
+    f, m = orc.spectrum(g["spec_x"].astype(np.float64), 72000, window=1 << 15)
+    np.testing.assert_array_equal(f, g["spec_f"])
+    assert np.max(np.abs(m - g["spec_m"])) <= 1e-6 * np.max(g["spec_m"])
+
+
 def test_spectrum_exact():
     g = golden("spectrum")
     for i, n in enumerate(g["lengths"]):
