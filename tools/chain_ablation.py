@@ -1,0 +1,78 @@
+"""Ablation builds of the single-pass chain kernel (tuning experiments only):
+patches csrc/chain_tile.hip into build/var/chain_tile_abl.hip with one phase
+removed per -D flag and links lib/libdspcore_<NAME>.so from it and the other
+objects of the in-tree build.  Time them with tools/gpu_libs.sh.
+
+    python tools/chain_ablation.py [NAME ...]   (default: all)
+
+NOSRC   y = window samples (no SRC FMAs)     NOP1  no pass-1 sums
+NOSCAN  no carry scan                        NOP2  no pass-2 cascade
+NOYST   no y store                           NOZST no z store (also lets the
+        compiler drop most of pass 2: read it together with NOP2)
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dsp-audio-project_amd", "csrc")
+BUILD = os.path.join(ROOT, "dsp-audio-project_amd", "build")
+LIB = os.path.join(ROOT, "dsp-audio-project_amd", "lib")
+HIPCC = "/opt/rocm/bin/hipcc"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vectorize",
+         f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+ALL = ["BASE", "NOSRC", "NOP1", "NOSCAN", "NOP2", "NOYST", "NOZST"]
+
+
+def patched() -> str:
+    s = open(os.path.join(CSRC, "chain_tile.hip")).read()
+
+    def rep(old, new):
+        nonlocal s
+        if old not in s:
+            raise SystemExit(f"chain_tile.hip changed; update the ablation patch near: {old[:60]!r}")
+        s = s.replace(old, new, 1)
+
+    parts = "".join(f"    src_part<GEO, {h}, 12>(xw, mt, y);\n    pin(y);\n" for h in (0, 12, 24, 36))
+    rep(parts, "#ifdef V_NOSRC\n#pragma unroll\n    for (int i = 0; i < TS; ++i) y[i] = xw[i];\n"
+        "    pin(y);\n#else\n" + parts + "#endif\n")
+    rep("#pragma unroll\n  for (int i = 0; i < TS; ++i) {\n    const double u = (double)y[i];",
+        "#ifdef V_NOP1\n#pragma unroll\n  for (int d = 0; d < kD; ++d) v[d] = (double)y[d];\n"
+        "  if (false)\n#endif\n#pragma unroll\n  for (int i = 0; i < TS; ++i) {\n"
+        "    const double u = (double)y[i];")
+    rep("#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {",
+        "#ifndef V_NOSCAN\n#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {")
+    rep("  // Entry state of the lane's sub-chunk", "#endif\n  // Entry state of the lane's sub-chunk")
+    rep("  store_tile<GEO>(lds, y, lane, ry, m0);\n",
+        "#ifndef V_NOYST\n  store_tile<GEO>(lds, y, lane, ry, m0);\n#endif\n")
+    rep("  {\n    double pend[kS];",
+        "#ifdef V_NOP2\n  for (int t = 0; t < TS; ++t) y[t] = clip_f32(y[t] + (float)s1[t % kS], lo, hi);\n"
+        "  if (false)\n#endif\n  {\n    double pend[kS];")
+    rep("  store_tile<GEO>(lds, y, lane_z, rz, m0);",
+        "#ifndef V_NOZST\n  store_tile<GEO>(lds, y, lane_z, rz, m0);\n#else\n"
+        "  if (y[0] == 12345.f) a.z[0] = y[1];\n#endif")
+    return s
+
+
+def main(names):
+    os.makedirs(os.path.join(BUILD, "var"), exist_ok=True)
+    src = os.path.join(BUILD, "var", "chain_tile_abl.hip")
+    with open(src, "w") as f:
+        f.write(patched())
+    others = [os.path.join(BUILD, f"{n}.o") for n in ("abi", "src_poly", "iir", "fft", "audio_io")]
+    procs = []
+    for name in names:
+        obj = os.path.join(BUILD, "var", f"chain_tile_{name}.o")
+        d = [] if name == "BASE" else [f"-DV_{name}"]
+        cmd = (f"{HIPCC} {' '.join(FLAGS + d)} -c {src} -o {obj} && "
+               f"{HIPCC} --offload-arch=gfx950 -shared -fPIC -o {LIB}/libdspcore_{name}.so "
+               f"{' '.join(others)} {obj}")
+        procs.append((name, subprocess.Popen(cmd, shell=True)))
+    for name, p in procs:
+        if p.wait():
+            raise SystemExit(f"build {name} failed")
+        print("built", name)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ALL)

@@ -1,0 +1,92 @@
+"""Same-box A/B of library builds (DSPCORE_LIB) on the single-pass chain:
+per-kernel HIP-event means over K traced steps and whole-step time, plus rows
+of y and z saved for a bitwise/tolerance comparison between builds.
+
+    DSPCORE_LIB=... python tools/tile_ab.py --tag NAME [--config c3] [--channels B ...]
+    python tools/tile_ab.py --compare TAG_A TAG_B
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "dsp-audio-project_amd"), ROOT]
+OUT = os.path.join(ROOT, "gpurun_out", "ab")
+
+import numpy as np  # noqa: E402
+
+
+def run(args):
+    import torch
+    from bench import CONFIG3_GAINS, WORKLOADS
+    from dspcore import _lib
+    from dspcore.chain import Chain, ChainConfig
+
+    os.makedirs(OUT, exist_ok=True)
+    wl = dict(WORKLOADS[args.config])
+    dev = torch.device("cuda", 0)
+    cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], CONFIG3_GAINS,
+                      n_fft=wl["n_fft"])
+    for B in args.channels:
+        ch = Chain(cfg, B, dev)
+        g = torch.Generator(device=dev).manual_seed(1234)
+        x = torch.rand((B, wl["n_in"]), device=dev, generator=g) * 2 - 1
+        for _ in range(3):
+            ch.run(x)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            ch.run(x)
+        e1.record()
+        torch.cuda.synchronize()
+        step_ms = e0.elapsed_time(e1) / args.steps
+        _lib.trace_enable(True)
+        _lib.trace_read()
+        for _ in range(args.steps):
+            ch.run(x)
+        recs = _lib.trace_read()
+        _lib.trace_enable(False)
+        per = {}
+        for k, ms in recs:
+            per.setdefault(k, []).append(ms)
+        rows = sorted({0, 1, B // 2, B - 1})
+        np.savez(os.path.join(OUT, f"{args.tag}_{B}.npz"), rows=np.array(rows),
+                 y=ch.y[rows].cpu().numpy(), z=ch.z[rows].cpu().numpy(),
+                 mag=ch.mag[rows].cpu().numpy())
+        print(json.dumps({"tag": args.tag, "B": B, "tile_len": ch.tile_len, "handoff_ok": ch.handoff_ok(),
+                          "step_ms": round(step_ms, 4),
+                          "kernels_ms": {k: round(float(np.mean(v)), 4) for k, v in per.items()}}),
+              flush=True)
+        del ch, x
+        torch.cuda.empty_cache()
+
+
+def compare(a, b):
+    for fa in sorted(os.listdir(OUT)):
+        if not fa.startswith(a + "_"):
+            continue
+        fb = os.path.join(OUT, b + fa[len(a):])
+        if not os.path.exists(fb):
+            continue
+        A, Bz = np.load(os.path.join(OUT, fa)), np.load(fb)
+        dy = float(np.max(np.abs(A["y"] - Bz["y"])))
+        dz = float(np.max(np.abs(A["z"] - Bz["z"])))
+        dm = float(np.max(np.abs(A["mag"] - Bz["mag"])) / max(1e-30, float(np.max(np.abs(A["mag"])))))
+        print(f"{fa[len(a) + 1:-4]}: y max|d| {dy:.3g} (bitwise {np.array_equal(A['y'], Bz['y'])}), "
+              f"z max|d| {dz:.3g}, mag rel {dm:.3g}")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--channels", type=int, nargs="+", default=[4096, 32768])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--compare", nargs=2)
+    args = ap.parse_args()
+    if args.compare:
+        compare(*args.compare)
+    else:
+        run(args)
