@@ -193,8 +193,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
   if (B == 0) return DSP_OK;
   int rc = dsp::kNotFused;
   if (dsp::g_chain_path == 0)
-    rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, K, L, M, c_offset, sos_host,
-                                S, clip, tile_tables, workspace, workspace_bytes, s);
+    rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
+                                sos_host, S, clip, tile_tables, workspace, workspace_bytes, s);
   if (rc == dsp::kNotFused) {
     // Two-launch chain: SRC, then the cascade with x-domain chunk states where
     // the input rows are aligned and the chunking fits, else the y-domain

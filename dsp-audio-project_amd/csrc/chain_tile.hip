@@ -142,6 +142,10 @@ struct TileArgs {
   uint32_t* err;            // set when a hand-off wait gave up
   int64_t B, n_in, ld_x, n_out, ld_y, ntiles, cq;
   int clip;
+  // generic kernel (k_chain_gen) only
+  const float* taps;        // device taps [K]
+  int64_t c;                // 'same' offset of the expanded convolution
+  int K, L, M, T, win;      // win: floats of one wave's x window
   SosParams p;
 };
 
@@ -226,15 +230,15 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
   for (int i = 0; i < NH; ++i) y[H0 + i] = acc[i].x + acc[i].y;
 }
 
-// Stores the tile's 64 x TSUB outputs (lane l holds outputs l*TSUB + i) as
+// Stores the tile's 64 x TS outputs (lane l holds outputs l*TS + i) as
 // coalesced float4s: each half of the lanes writes its rows into LDS (row
-// stride TSUB + 4: conflict-free ds_write_b128), then all 64 lanes store the
-// half's contiguous 32*TSUB floats.  Stores past the row's end are dropped by
-// the buffer resource.
-template <class GEO>
-__device__ __forceinline__ void store_tile(float* lds, const float (&v)[GEO::TSUB], int lane,
+// stride TS + 4: conflict-free ds_write_b128), then all 64 lanes store the
+// half's contiguous 32*TS floats.  The buffer resource checks every dword:
+// stores past the row's end are dropped, a float4 across it keeps its head.
+template <int TS>
+__device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int lane,
                                            __amdgpu_buffer_rsrc_t rs, int64_t m0) {
-  constexpr int TS = GEO::TSUB, RS = GEO::RS;
+  constexpr int RS = TS + 4;
   constexpr int NF4 = (kWave / 2) * TS / 4;
   static_assert(NF4 % kWave == 0, "whole float4 rounds per half");
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -266,50 +270,16 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[GEO::TSU
   fence();
 }
 
-template <class GEO>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
-    TileArgs a) {
-  constexpr int TS = GEO::TSUB;
-  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
-  const int lane = threadIdx.x;
-  const int64_t id = blockIdx.x;
-  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
-  const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
-  const tt_ptr mt = (tt_ptr)a.tt;  // wave-uniform: scalar loads
+// LDS floats store_tile<TS> stages through.
+__host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * (ts + 4); }
 
-  // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
-  {
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
-    const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);  // multiple of 4
-    constexpr int NF = GEO::NWIN / 4;
-#pragma unroll
-    for (int k = 0; k < (NF + kWave - 1) / kWave; ++k) {
-      const int f = lane + kWave * k;
-      if ((k + 1) * kWave <= NF || f < NF) {
-        // "Negative" offsets (tile 0) are >= 2^31 as unsigned: out of range, zeros.
-        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, 0);
-        *reinterpret_cast<f32x4*>(lds + xpad(4 * f)) = v;
-      }
-    }
-  }
-  fence();  // one wave: its LDS operations execute in order
-
-  // ---- 1. SRC: the lane's TSUB outputs, in parts of 12 (register pressure)
-  float y[TS];
-  {
-    const float* xw = lds + 36 * lane;
-    static_assert(TS == 48, "four parts");
-    src_part<GEO, 0, 12>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 12, 12>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 24, 12>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 36, 12>(xw, mt, y);
-    pin(y);
-  }
-
+// Steps 2-5 of the tile (file comment) for a wave that holds its y sub-chunk:
+// pass 1, entry state (hand-off) and scan, publish, y out, s = T m, pass 2,
+// z out.  lds: at least staging_floats(TS) floats the wave may overwrite.
+template <int TS>
+__device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
+                                             float (&y)[TS], int lane, int64_t b, int64_t tile,
+                                             int64_t m0) {
   // ---- 2. pass 1: zero-state end state of the sub-chunk, block-diagonal coords
   double v[kD];
 #pragma unroll
@@ -378,7 +348,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   // ---- 5. y out, DF2 entry state s = T m, pass 2, z out
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-  store_tile<GEO>(lds, y, lane, ry, m0);
+  store_tile<TS>(lds, y, lane, ry, m0);
   pin(y);
   double s1[kS], s2[kS];
 #pragma unroll
@@ -405,11 +375,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         const double u = k == 0 ? (double)y[t] * a.p.G : pend[k - 1];
         const double* cf = a.p.c[k];
         const double w = fma(-cf[4], s2[k], fma(-cf[3], s1[k], u));
-        const double v = fma(cf[2], s2[k], fma(cf[1], s1[k], w));
+        const double v2 = fma(cf[2], s2[k], fma(cf[1], s1[k], w));
         s2[k] = s1[k];
         s1[k] = w;
-        if (k == kS - 1) y[t] = clip_f32((float)v, lo, hi);
-        else pend[k] = v;
+        if (k == kS - 1) y[t] = clip_f32((float)v2, lo, hi);
+        else pend[k] = v2;
       }
     }
   }
@@ -417,7 +387,207 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   int lane_z = lane;
   asm volatile("" : "+v"(lane_z));  // recompute the store offsets (no spill across pass 2)
-  store_tile<GEO>(lds, y, lane_z, rz, m0);
+  store_tile<TS>(lds, y, lane_z, rz, m0);
+}
+
+template <class GEO>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
+    TileArgs a) {
+  constexpr int TS = GEO::TSUB;
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  const int lane = threadIdx.x;
+  const int64_t id = blockIdx.x;
+  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
+  const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
+  const tt_ptr mt = (tt_ptr)a.tt;  // wave-uniform: scalar loads
+
+  // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);  // multiple of 4
+    constexpr int NF = GEO::NWIN / 4;
+#pragma unroll
+    for (int k = 0; k < (NF + kWave - 1) / kWave; ++k) {
+      const int f = lane + kWave * k;
+      if ((k + 1) * kWave <= NF || f < NF) {
+        // "Negative" offsets (tile 0) are >= 2^31 as unsigned: out of range, zeros.
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, 0);
+        *reinterpret_cast<f32x4*>(lds + xpad(4 * f)) = v;
+      }
+    }
+  }
+  fence();  // one wave: its LDS operations execute in order
+
+  // ---- 1. SRC: the lane's TSUB outputs, in parts of 12 (register pressure)
+  float y[TS];
+  {
+    const float* xw = lds + 36 * lane;
+    static_assert(TS == 48, "four parts");
+    src_part<GEO, 0, 12>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 12, 12>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 24, 12>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 36, 12>(xw, mt, y);
+    pin(y);
+  }
+  tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
+}
+
+// ---------------------------------------------------------------------------
+// Generic single-pass kernel: any L, M with ceil(K/L) <= 8 (config 5's
+// L/M = 160/147, K = 1023: 7 taps per branch).  The polyphase branch of a
+// lane's outputs changes from output to output and from lane to lane, so the
+// SRC reads its taps and samples from LDS at run-time offsets instead of the
+// specialised kernel's wave-uniform scalar taps:
+//   j = m*M + c, phi = j mod L, q = j div L (incremental per output),
+//   y[m] = sum_u h[phi][u] x[q - (T-1) + u],  h[phi][u] = taps[phi + L(T-1-u)],
+// summed as k_src_generic does (even u into a0, odd u into a1, y = a0 + a1),
+// so y is bitwise that kernel's.  A workgroup is kGenWaves waves, one channel
+// each at the same tile index (ids stay tile-major for the hand-off); they
+// share the tap bank [L][8] in LDS.  Each wave owns its x window (and stages
+// its stores through it).  Steps 2-5 are tile_cascade<32>.
+// ---------------------------------------------------------------------------
+constexpr int kGenTS = 32;                    // outputs per lane
+constexpr int kGenTile = kWave * kGenTS;      // outputs per tile (wave)
+constexpr int kGenWaves = 4;                  // waves (channels) per workgroup
+constexpr int kGenTT = 8;                     // bank row: taps per branch (T <= 8)
+
+// Row phi of the tap bank: 8 floats, plus 4 floats of padding after every 32
+// rows, so that the branches lanes read together (phases 32 apart for config
+// 5: (32 l M + c) mod L with 32 M = 64 mod 160) start on distinct bank quads.
+__host__ __device__ constexpr int bank_row(int phi) { return phi * kGenTT + 4 * (phi >> 5); }
+__host__ __device__ constexpr int bank_floats(int L) { return bank_row(L) + 4; }
+
+template <bool UP>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gen(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* bank = smem;  // [L][kGenTT], rows at bank_row(phi)
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
+  const int64_t tile = blockIdx.x / groups;
+  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  const int L = a.L, M = a.M, T = a.T;
+  // Tap bank, 8 loads in flight per thread per round (a loop with one load per
+  // iteration would wait out one memory latency per element).
+  constexpr int kNT = kWave * kGenWaves;
+  for (int i0 = 0; i0 < L * kGenTT; i0 += 8 * kNT) {
+    float t[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = i0 + r * kNT + (int)threadIdx.x;
+      const int phi = i / kGenTT, u = i - phi * kGenTT;
+      const int k = phi + L * (T - 1 - u);
+      const float v = a.taps[k < 0 ? 0 : (k < a.K ? k : a.K - 1)];  // unconditional load
+      t[r] = (i < L * kGenTT && u < T && k < a.K) ? v : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = i0 + r * kNT + (int)threadIdx.x;
+      const int phi = i / kGenTT, u = i - phi * kGenTT;
+      if (i < L * kGenTT) bank[bank_row(phi) + u] = t[r];
+    }
+  }
+  __syncthreads();
+  if (b >= a.B) return;
+  const tt_ptr mt = (tt_ptr)a.tt;
+  float* win = smem + bank_floats(L) + w * a.win;
+  const int64_t m0 = tile * kGenTile;
+
+  // ---- x window of the tile: x[qa .. qa + nload) (zeros outside [0, n_in))
+  const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
+  const int64_t qa = (qlo >> 2) << 2;  // floor to a multiple of 4
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    // The whole window (taps past T read real samples), 8 float4 loads in
+    // flight per lane per round.
+    const int nf = a.win >> 2;
+    for (int f0 = 0; f0 < nf; f0 += 8 * kWave) {
+      f32x4 v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kWave + lane;  // past the window: harmless reads
+        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kWave + lane;
+        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+      }
+    }
+  }
+  fence();
+
+  // ---- 1. SRC of the lane's 32 outputs, software-pipelined one output deep
+  // (output i+1's LDS reads are issued before output i's FMAs).  UP (M < L):
+  // q advances by 0 or 1 per output, so the 8-sample window slides in
+  // registers and one new sample is read per output; otherwise all 8 are read.
+  float y[kGenTS];
+  {
+    const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
+    const int64_t q0 = j0 / L;
+    int phi = (int)(j0 - q0 * L);
+    int qr = (int)(q0 - (T - 1) - qa);  // window offset of the output's first tap
+    const int dq = M / L, dphi = M - dq * L;
+    float w[kGenTT];
+#pragma unroll
+    for (int u = 0; u < kGenTT; ++u) w[u] = win[qr + u];
+    const float* hr = bank + bank_row(phi);
+    float4 h0 = *reinterpret_cast<const float4*>(hr);
+    float4 h1 = *reinterpret_cast<const float4*>(hr + 4);
+    float nx = UP ? win[qr + kGenTT] : 0.f;  // enters the window if q advances
+#pragma unroll
+    for (int i = 0; i < kGenTS; ++i) {
+      // indices and operands of output i+1
+      int phi_n = phi + dphi, qr_n = qr + dq;
+      const bool carry = phi_n >= L;
+      phi_n = carry ? phi_n - L : phi_n;
+      qr_n = carry ? qr_n + 1 : qr_n;
+      float4 h0n, h1n;
+      float nxn = 0.f, wn[kGenTT];
+      if (i + 1 < kGenTS) {
+        const float* hrn = bank + bank_row(phi_n);
+        h0n = *reinterpret_cast<const float4*>(hrn);
+        h1n = *reinterpret_cast<const float4*>(hrn + 4);
+        if constexpr (UP) {
+          nxn = win[qr_n + kGenTT];
+        } else {
+#pragma unroll
+          for (int u = 0; u < kGenTT; ++u) wn[u] = win[qr_n + u];
+        }
+      }
+      // (even u, odd u) partial sums in the halves of one v_pk_fma_f32
+      // chain: the same two chains, in the same order, as k_src_generic's.
+      f32x2 acc = {0.f, 0.f};
+      acc = __builtin_elementwise_fma(f32x2{h0.x, h0.y}, f32x2{w[0], w[1]}, acc);
+      acc = __builtin_elementwise_fma(f32x2{h0.z, h0.w}, f32x2{w[2], w[3]}, acc);
+      acc = __builtin_elementwise_fma(f32x2{h1.x, h1.y}, f32x2{w[4], w[5]}, acc);
+      acc = __builtin_elementwise_fma(f32x2{h1.z, h1.w}, f32x2{w[6], w[7]}, acc);
+      y[i] = acc.x + acc.y;
+      if (i + 1 < kGenTS) {
+        if constexpr (UP) {
+#pragma unroll
+          for (int u = 0; u < kGenTT - 1; ++u) w[u] = carry ? w[u + 1] : w[u];
+          w[kGenTT - 1] = carry ? nx : w[kGenTT - 1];
+          nx = nxn;
+        } else {
+#pragma unroll
+          for (int u = 0; u < kGenTT; ++u) w[u] = wn[u];
+        }
+        h0 = h0n;
+        h1 = h1n;
+        phi = phi_n;
+        qr = qr_n;
+      }
+    }
+  }
+  pin(y);
+  tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
 }
 
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
@@ -425,22 +595,54 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 typedef TileGeo<3, 2, 41, 0> Geo3241;
 
 struct TilePlan {
+  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen
   int64_t tsub, tile, ntiles;
+  int win;   // kind 2: floats of a wave's x window
 };
+
+// Floats of the generic kernel's x window for one tile: the tile's input span
+// ((kGenTile-1) M / L + T), up to 3 of alignment, and taps past T reading up
+// to kGenTT - T samples beyond; at least the store staging.
+int gen_window(int L, int M, int T) {
+  const int64_t w = ((int64_t)(kGenTile - 1) * M) / L + T + 4 + (kGenTT - T) + 2;
+  const int64_t r = (w + 3) / 4 * 4;
+  return (int)std::max<int64_t>(r, staging_floats(kGenTS));
+}
+
+size_t gen_lds_bytes(int L, int win) {
+  return ((size_t)bank_floats(L) + (size_t)kGenWaves * win) * sizeof(float);
+}
+constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
 
 bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
                    TilePlan* tp) {
-  const int TT = (K + L - 1) / L;
-  if (!(L == 3 && M == 2 && TT == 41 && c % L == 0)) return false;
-  if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || n_out % 4) return false;
+  if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
+  if (L == 1 && M == 1) return false;  // SRC bypass: the caller's cascade path
   if (n_in * 4 + 16 >= ((int64_t)1 << 31) || n_out * 4 + 16 >= ((int64_t)1 << 31)) return false;
-  // Lane windows on 16-byte boundaries: x offset of tile t's window is
-  // t*2048 + c/L - (TT-1), a multiple of 4 iff c/L - (TT-1) is.
-  if (((c / L) - (TT - 1)) % 4 != 0) return false;
-  tp->tsub = Geo3241::TSUB;
-  tp->tile = Geo3241::TILE;
-  tp->ntiles = ceil_div(n_out, tp->tile);
-  return true;
+  const int TT = (K + L - 1) / L;
+  // Specialised kernel: lane windows on 16-byte boundaries, i.e. the x offset
+  // of tile t's window, t*2048 + c/L - (TT-1), a multiple of 4.
+  if (L == 3 && M == 2 && TT == 41 && c % L == 0 && n_out % 4 == 0 &&
+      ((c / L) - (TT - 1)) % 4 == 0) {
+    tp->kind = 1;
+    tp->tsub = Geo3241::TSUB;
+    tp->tile = Geo3241::TILE;
+    tp->ntiles = ceil_div(n_out, tp->tile);
+    tp->win = 0;
+    return true;
+  }
+  if (TT <= kGenTT && L <= 4096) {
+    const int win = gen_window(L, M, TT);
+    if (gen_lds_bytes(L, win) <= kGenLdsMax) {
+      tp->kind = 2;
+      tp->tsub = kGenTS;
+      tp->tile = kGenTile;
+      tp->ntiles = ceil_div(n_out, tp->tile);
+      tp->win = win;
+      return true;
+    }
+  }
+  return false;
 }
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -635,9 +837,9 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   TileTables* tt = static_cast<TileTables*>(out);
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
-  tap_pairs<Geo3241>(taps, K, tt);
+  if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);  // kind 2 reads the device taps
   tt->tsub = (int32_t)tp.tsub;
-  tt->np = Geo3241::NP;
+  tt->np = tp.kind == 1 ? Geo3241::NP : 0;
   tt->L = L;
   tt->M = M;
   tt->K = K;
@@ -646,8 +848,8 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
 }
 
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
-                      int64_t n_out, int64_t ld_y, int K, int L, int M, int64_t c,
-                      const double* sos, int S, int clip, const void* tables, void* ws,
+                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
+                      int64_t c, const double* sos, int S, int clip, const void* tables, void* ws,
                       size_t ws_bytes, hipStream_t s) {
   TilePlan tp;
   if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
@@ -681,11 +883,28 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.ntiles = tp.ntiles;
   a.cq = c / L;
   a.clip = clip;
+  a.taps = taps;
+  a.c = c;
+  a.K = K;
+  a.L = L;
+  a.M = M;
+  a.T = (K + L - 1) / L;
+  a.win = tp.win;
   a.p = p;
-  {
+  if (tp.kind == 1) {
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,
                        a);
+  } else {
+    DSP_REQUIRE(taps, "null taps");
+    const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
+    DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
+    const size_t shm = gen_lds_bytes(L, tp.win);
+    auto kern = M < L ? k_chain_gen<true> : k_chain_gen<false>;
+    if (int rc = allow_lds(kern, shm)) return rc;
+    TraceScope trace("chain_tile", s);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
+                       s, a);
   }
   DSP_LAUNCHED("k_chain_tile");
   return DSP_OK;

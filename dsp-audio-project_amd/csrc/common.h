@@ -122,8 +122,8 @@ size_t chain_tile_tables_bytes();
 int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, const float* taps,
                       int K, int L, int M, int64_t c, const double* sos, int S);
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
-                      int64_t n_out, int64_t ld_y, int K, int L, int M, int64_t c,
-                      const double* sos, int S, int clip, const void* tables, void* ws,
+                      int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
+                      int64_t c, const double* sos, int S, int clip, const void* tables, void* ws,
                       size_t ws_bytes, hipStream_t s);
 // Whether launch_biquad_xstate's conditions on the cascade (n, S, chunk_len)
 // and on the SRC input rows (16-byte aligned) hold.

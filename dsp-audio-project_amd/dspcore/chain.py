@@ -80,8 +80,14 @@ class Chain:
         self.window = ops._table("hann", self.spec.n_fft, dev)
         self.tw = ops._table("tw", self.spec.n_fft, dev)
         self.sos = np.ascontiguousarray(self.eq.sos, dtype=np.float64)
-        self.y = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
-        self.z = torch.empty((self.B, n_out), dtype=torch.float32, device=dev)
+        # Rows on 16-byte boundaries (pitch a multiple of 4 floats) so that the
+        # single-pass kernel's float4 stores apply to every n_out; y and z are
+        # [B, n_out] views of the padded buffers.
+        ld = -(-n_out // 4) * 4
+        self._ybuf = torch.empty((self.B, ld), dtype=torch.float32, device=dev)
+        self._zbuf = torch.empty((self.B, ld), dtype=torch.float32, device=dev)
+        self.y = self._ybuf[:, :n_out]
+        self.z = self._zbuf[:, :n_out]
         self.mag = torch.empty((self.B, self.spec.n_fft // 2 + 1), dtype=torch.float32,
                                device=dev)
         ws_bytes = lib.dsp_chain_workspace_bytes(self.B, cfg.n_in, n_out, self.src.K, self.src.L,

@@ -79,8 +79,12 @@ def _rows(x: torch.Tensor, name: str) -> torch.Tensor:
 
 
 def ld(x: torch.Tensor) -> int:
-    """Row pitch in elements (a single row's stride(0) is meaningless)."""
-    return x.stride(0) if x.shape[0] > 1 else x.shape[1]
+    """Row pitch in elements.  A single row's stride(0) is only a pitch when it
+    covers the row (a [1, n] view of a padded buffer keeps its padded pitch,
+    which the aligned kernels need); otherwise the row length stands in."""
+    if x.shape[0] > 1:
+        return x.stride(0)
+    return x.stride(0) if x.stride(0) >= x.shape[1] else x.shape[1]
 
 
 def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:

@@ -140,9 +140,10 @@ def test_wav_header_matches_scipy_writer():
 
 def test_chain_path_tile_len_and_workspace_query():
     """dsp_chain_path takes 0/1 (-1 queries); dsp_chain_tile_len names the
-    single-pass geometry (config 3's L3/M2, K = 121: 48-sample sub-chunks) and
+    single-pass geometries (config 3's L3/M2, K = 121: 48-sample sub-chunks;
+    any L/M with ceil(K/L) <= 8, e.g. config 5's 160/147, K = 1023: 32) and
     declines others; the chain workspace holds the tile hand-off (a 12-double
-    state and a flag per tile, 3072-output tiles) or the two-launch
+    state and a flag per tile, 3072- or 2048-output tiles) or the two-launch
     cascade's scratch, whichever is larger."""
     lib = _lib.load()
     prev = lib.dsp_chain_path(-1)
@@ -152,13 +153,17 @@ def test_chain_path_tile_len_and_workspace_query():
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 6) == 48
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 3) == 48   # padded stages
     assert lib.dsp_chain_tile_len(47996, 71994, 121, 3, 2, 60, 6) == 0    # n_out % 4
-    assert lib.dsp_chain_tile_len(48000, 52245, 1023, 160, 147, 511, 6) == 0
+    assert lib.dsp_chain_tile_len(48000, 52245, 1023, 160, 147, 511, 6) == 32   # generic
+    assert lib.dsp_chain_tile_len(48000, 52245, 6401, 160, 147, 3200, 6) == 0   # 41 taps/branch
+    assert lib.dsp_chain_tile_len(47999, 52244, 1023, 160, 147, 511, 6) == 0    # n_in % 4
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 7) == 0    # > 6 stages
     B, n_in, n_out = 4096, 48000, 72000
     tiles = -(-n_out // 3072)
     ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)
     assert ws >= B * tiles * (12 * 8 + 4)
-    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 1023, 160, 147, 511, 6, 1152) == 0
+    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 1023, 160, 147, 511, 6, 1152) >= \
+        B * -(-52245 // 2048) * (12 * 8 + 4)
+    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 6401, 160, 147, 3200, 6, 1152) == 0
 
 
 def test_chain_tile_tables_host_only():
@@ -166,8 +171,8 @@ def test_chain_tile_tables_host_only():
     block-diagonal carry tables reproduce the cascade's dense state algebra
     (T D^(48 2^d) T^-1 = A^(48 2^d); T sum_i G'[i] y[i] = the zero-state end
     state of a 48-sample sub-chunk) and the tap pairs are the reversed
-    polyphase branches shifted by their window parity; other geometries
-    decline with 1."""
+    polyphase branches shifted by their window parity; config 5's geometry
+    builds 32-sample tables for the generic kernel; others decline with 1."""
     import numpy as np
 
     from dspcore import design
@@ -211,5 +216,23 @@ def test_chain_tile_tables_host_only():
     assert not TP[21:].any() and not TP[:, 3].any()
     c5 = design.src_plan(48000, 44100, 147, 160, 1023)
     t5 = np.ascontiguousarray(c5.taps, dtype=np.float32)
+    # config 5 (generic kernel): 32-sample sub-chunks, no tap pairs (the kernel
+    # reads the device taps); 41 taps per branch declines with 1.
+    sos5 = np.ascontiguousarray(design.eq_plan(c5.fs_out, gains).sos)
+    buf[:] = 0
     assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c5.n_out, t5.ctypes.data,
-                                     c5.K, 160, 147, c5.c_offset, _lib.sos_pointer(sos), 6) == 1
+                                     c5.K, 160, 147, c5.c_offset, _lib.sos_pointer(sos5), 6) == 0
+    assert tuple(buf[9472:].view(np.int32)) == (32, 0, 160, 147, 1023, 6)
+    G5 = buf[:6144].view(np.float64).reshape(64, 12)
+    T5 = buf[7296:8448].view(np.float64).reshape(12, 12)
+    A5, B5 = design.state_space(sos5)
+    y = np.random.default_rng(1).uniform(-1, 1, 32)
+    X = np.zeros(12)
+    for v in y:
+        X = A5 @ X + B5 * v
+    np.testing.assert_allclose(T5 @ (G5[:32].T @ y), X, rtol=1e-10, atol=1e-12)
+    assert not buf[8448:9472].any()
+    c6 = design.src_plan(48000, 44100, 147, 160)
+    t6 = np.ascontiguousarray(c6.taps, dtype=np.float32)
+    assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c6.n_out, t6.ctypes.data,
+                                     c6.K, 160, 147, c6.c_offset, _lib.sos_pointer(sos5), 6) == 1

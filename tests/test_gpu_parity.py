@@ -447,6 +447,49 @@ def test_chain_single_pass_matches_two_launch(gpu, n_in, tile):
         assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
 
 
+@pytest.mark.parametrize("n_in,fs,L,M,K,B", [(48000, 44100, 160, 147, 1023, 6),
+                                             (4800, 44100, 160, 147, 1023, 3),
+                                             (9000, 48000, 5, 4, 31, 5),
+                                             (6600, 48000, 2, 3, 15, 9),
+                                             (4000, 48000, 7, 3, 55, 4)])
+def test_chain_generic_single_pass(gpu, n_in, fs, L, M, K, B):
+    """The generic single-pass kernel (k_chain_gen: run-time L/M, ceil(K/L) <=
+    8, e.g. config 5's 160/147 with K = 1023) against the two-launch chain:
+    it ran where dsp_chain_tile_len says so, y bitwise the generic SRC kernel's
+    (same summation order), z within float64 rounding, odd n_out (ragged float4
+    at the row end), batches that leave waves of the last workgroup idle,
+    up- and down-sampling; rows against the reference recipe."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    n_fft = 4096 if n_in >= 10000 else 2048
+    cfg = ChainConfig(n_in, fs, L, M, K, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 32
+    gen = torch.Generator(device=gpu).manual_seed(11)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[1] *= 40.0                      # drive the clip
+    x[2, : n_in // 2] = 0.0           # silence then signal
+    (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
+    with _chain_path(1):
+        (y0, z0, m0), names0 = _traced(lambda: ch.run(x))
+    assert "chain_tile" in names1 and "src_poly" not in names1, names1
+    assert "chain_tile" not in names0, names0
+    assert ch.handoff_ok()
+    assert torch.equal(y1, y0)
+    assert (z1 - z0).abs().max().item() <= 2e-6
+    assert (m1 - m0).abs().max().item() <= 1e-5 * m0.abs().max().item()
+    y, z, mag = (t.cpu().numpy() for t in (y1, z1, m1))
+    assert np.abs(z[1]).max() == 1.0
+    for b in (0, 1, 2, B - 1):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), fs, L, M, orc.CONFIG3_GAINS, K, n_fft)
+        assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+    # more than 8 taps per branch: the two-launch chain serves the call
+    assert Chain(ChainConfig(n_in, fs, L, M, 17 * L, orc.CONFIG3_GAINS, n_fft=n_fft), 1,
+                 gpu).tile_len == 0
+
+
 @pytest.mark.parametrize("gains", [{"Sub-Bass": 6, "Bass": 0.0, "Presence": -3, "Otra": 4},
                                    {"Sub-Bass": 0, "Bass": 0.05}])
 def test_chain_single_pass_fewer_bands_and_bypass(gpu, gains):
@@ -544,8 +587,8 @@ def test_shards_plan_with_the_job_batch(gpu):
     def fn(plan):
         def run(xd):
             ch = Chain(cfg, xd.shape[0], xd.device, plan_batch=plan)
-            assert ch.tile_len == 0
-            y, z, mag = ch.run(xd)
+            with _chain_path(1):          # the two-launch chain (its chunking is planned)
+                y, z, mag = ch.run(xd)
             return z.clone(), mag.clone()
         return run
 

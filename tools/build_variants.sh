@@ -10,7 +10,7 @@ while [ $# -ge 2 ]; do
   for f in abi src_poly iir chain_tile fft audio_io; do
     if [ "$f" = "$src" ]; then objs="$objs ../build/var/${f}_$name.o"; else objs="$objs ../build/$f.o"; fi
   done
-  extra=""; [ "$src" = iir ] && extra="-fno-slp-vectorize"
+  extra=""; { [ "$src" = iir ] || [ "$src" = chain_tile ]; } && extra="-fno-slp-vectorize"
   ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -I. $extra $flags -c $src.hip -o ../build/var/${src}_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/libdspcore_$name.so $objs && echo built $name ) &
 done
