@@ -77,13 +77,13 @@ __device__ __forceinline__ double cascade_step(double u, double (&w1)[S > 0 ? S 
   return u;
 }
 
-// np.clip(v, lo, hi) with NaN kept (v_med3_f32 maps NaN to a bound).
-// Clipping after the float32 rounding gives the same result as rounding the
-// float64 clip (|v| <= 1 rounds to |v| <= 1, anything beyond rounds to
-// beyond-or-equal).  lo/hi = -inf/+inf is the identity.
+// np.clip(v, lo, hi) with NaN kept: IEEE 754-2019 maximum/minimum propagate
+// NaN (v_maximum3_f32 / v_minimum3_f32 on gfx950, two VALU).  Clipping after
+// the float32 rounding gives the same result as rounding the float64 clip
+// (|v| <= 1 rounds to |v| <= 1, anything beyond rounds to beyond-or-equal).
+// lo/hi = -inf/+inf is the identity.
 __device__ __forceinline__ float clip_f32(float v, float lo, float hi) {
-  const float m = __builtin_amdgcn_fmed3f(v, lo, hi);
-  return v != v ? v : m;
+  return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, lo), hi);
 }
 
 // One step of the realisation's state with input u: X <- A X + B u.  Host

@@ -350,12 +350,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   store_tile<TS>(lds, y, lane, ry, m0);
   pin(y);
+  // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
+  // rows and columns for padding stages), so row r starts from m[r].
   double s1[kS], s2[kS];
 #pragma unroll
   for (int r = 0; r < kD; ++r) {
-    double acc = 0.0;
+    double acc = m[r];
 #pragma unroll
-    for (int cc = 0; cc < (r / 2 + 1) * 2; ++cc) acc = fma(mt->T[r][cc], m[cc], acc);
+    for (int cc = 0; cc < (r / 2) * 2; ++cc) acc = fma(mt->T[r][cc], m[cc], acc);
     if (r & 1) s2[r / 2] = acc;
     else s1[r / 2] = acc;
   }

@@ -160,15 +160,20 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * call leaves it ready for the next one.  Each row's result is bitwise
  * independent of B.
  *
- * Single-pass path (default).  When dsp_chain_tile_len() is nonzero (today:
- * (L, M, ceil(K/L)) = (3, 2, 41) with c_offset mod 3 == 0 and
- * (c_offset/3 - 40) mod 4 == 0, S <= 6 with every b0 != 0, n_in and n_out
- * multiples of 4), `tile_tables` is a device copy (256-byte aligned) of the
- * tables dsp_chain_tile_tables built for this call's geometry, taps and sos,
- * and the rows of x, y and z are 16-byte aligned with pitches that are
- * multiples of 4, ONE kernel computes y and z from x: x is read once, y and z
- * are written once, y is never read back.  Its y is bitwise that of
- * dsp_src_polyphase_f32; z equals the two-launch chain's to float64 rounding.
+ * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
+ * S <= 6 with every b0 != 0, n_in a multiple of 4, not the SRC bypass, and
+ *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
+ *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
+ *       with wave-uniform taps: configs 3 and 4), or
+ *   32: any other L/M with ceil(K/L) <= 8 whose tap bank and four x windows
+ *       fit 64 KB of LDS (run-time taps: config 5's 160/147, K = 1023),
+ * `tile_tables` is a device copy (256-byte aligned) of the tables
+ * dsp_chain_tile_tables built for this call's geometry, taps and sos, and the
+ * rows of x, y and z are 16-byte aligned with pitches that are multiples of 4
+ * (n_out itself need not be), ONE kernel computes y and z from x: x is read
+ * once, y and z are written once, y is never read back.  Its y is bitwise
+ * that of dsp_src_polyphase_f32; z equals the two-launch chain's to float64
+ * rounding.
  * chunk_len, state_table and xstate_table are not used by it.  Workspace word
  * 0 (uint32) is nonzero after a call whose tile hand-off wait gave up (a broken
  * dispatch order; z is then wrong): a diagnostic, normally 0.
@@ -177,8 +182,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * (>= dsp_chain_tile_tables_bytes()) with the single-pass kernel's float64
  * carry tables (the cascade in block-diagonal coordinates: the sub-chunk
  * state-response rows, the powers of the diagonal blocks, the change of basis)
- * and its packed tap pairs, from the HOST float32 taps (the same values as
- * `taps`) and sos.  Returns 0 when the single-pass kernel serves the geometry
+ * and, for the 48-sample kernel, its packed tap pairs, from the HOST float32
+ * taps (the same values as `taps`, which the 32-sample kernel reads) and sos.  Returns 0 when the single-pass kernel serves the geometry
  * (copy the buffer to the device once and pass it to every call), 1 when it
  * does not (the two-launch path serves it; nothing to copy), DSP_EINVAL on bad
  * arguments.  With tile_tables == NULL dsp_chain_f32 takes the two-launch path.
