@@ -47,6 +47,7 @@ for _p in (os.path.join(ROOT, "dsp-audio-project_amd"), ROOT):
 
 METRIC = "Msamples/sec SRC→6-biquad EQ→FFT chain at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector peak (FMA = 2 flops)
 CONFIG3_GAINS = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3,
                  "High Mids": -3, "Presence": 5, "Brilliance": -6}
 
@@ -178,6 +179,24 @@ def kernel_bytes(chain, name):
     }.get(name, 0)
 
 
+def valu_work(chain, mean_ms):
+    """float64 FMA work of the single-pass kernel, the
+    resource that binds it: per output sample 12 (pass 1) + 24 (pass 2), plus
+    the per-tile carry per TS-sample sub-chunk (6 scan levels x 24, s = T m 72,
+    the entry state 24 = 240 per lane).  None for the two-launch chain."""
+    ts = chain.tile_len
+    if not ts:
+        return None
+    per_sample = 36 + 240 / ts
+    fma = per_sample * chain.B * chain.n_out
+    tflops = 2 * fma / (mean_ms * 1e-3) / 1e12
+    return {"bound": "valu (fp64 FMA issue)", "fp64_fma_per_output_sample": round(per_sample, 3),
+            "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
+            "note": "the kernel also issues 21 (L3/M2) or 4 (generic) v_pk_fma_f32 per sample for "
+                    "the SRC; profiles/r02_chain_ablation.txt: ~83 % VALU issue efficiency"}
+
+
 def load_traffic(wl_name, channels):
     """PMC HBM bytes per launch for this workload and batch, from the summary
     tools/pmc_parse.py --write keeps in profiles/pmc_traffic.json."""
@@ -298,6 +317,7 @@ def main(argv=None):
     achieved = r["dom_bytes"] / (mean_ms * 1e-3) / 1e9
     traffic_map, traffic_src = load_traffic(wl["name"], B)
     traffic = traffic_map.get(dom)
+    valu = valu_work(chain, mean_ms) if dom == "chain_tile" else None
     chain_bytes = chain.algorithmic_bytes()
     chain_gbs = chain_bytes / (ms_per_step * 1e-3) / 1e9
     launch, n_out, dom_bytes = r["launch"], chain.n_out, r["dom_bytes"]
@@ -349,6 +369,7 @@ def main(argv=None):
                 "traffic_source": traffic_src if traffic else None,
                 "algorithmic_bytes": dom_bytes,
                 "mean_ms": mean_ms,
+                "valu": valu,
             },
             "chain_roofline": {
                 "achieved": round(chain_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
