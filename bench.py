@@ -306,7 +306,10 @@ def main(argv=None):
         import torch.distributed as tdist
         tdist.init_process_group("gloo")      # timing barrier + max only: no RCCL
         dist = tdist
-    device = torch.device("cuda", local_rank)
+    # DSP_BENCH_DEVICE pins every rank to one device: a rehearsal of the
+    # multi-rank path on a one-GPU box (the driver's runs leave it unset).
+    dev_index = int(os.environ.get("DSP_BENCH_DEVICE", local_rank))
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
 
     r = measure(wl, B, args.steps, args.warmup, rank, world, dist, args.eager, device)

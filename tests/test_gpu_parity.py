@@ -105,6 +105,19 @@ def test_src_drop_in_dtypes_and_identity(gpu):
     assert yt.is_cuda and yt.dtype == torch.float32
 
 
+def test_config2_full_length(gpu):
+    """BASELINE config 2 at its stated size: 1 channel x 48000 samples, 255-tap
+    FIR, L = 3 / M = 2, SRC only, through the drop-in against the oracle."""
+    from oracle import dsp_ref_cpu as orc
+    dc = _dc()
+    rng = np.random.default_rng(22)
+    x = rng.uniform(-1, 1, 48000).astype(np.float32)
+    y, fs_out = dc.conversion_tasa_muestreo(x, 48000, 2, 3, num_taps=255)
+    ry, rfs = orc.resample(x, 48000, 2, 3, 255)
+    assert fs_out == rfs == 72000 and y.shape == ry.shape == (72000,)
+    assert np.max(np.abs(y - ry)) <= SRC_ATOL
+
+
 def test_src_misaligned_rows_and_long_taps(gpu):
     from dspcore import design
     from oracle import dsp_ref_cpu as orc
