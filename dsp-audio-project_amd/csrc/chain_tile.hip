@@ -130,6 +130,12 @@ struct TileTables {
   double T[kD][kD];        // s = T m (row-major; zero rows/cols: padding stages)
   float TP[kNPMax][4][2];  // tap pairs: TP[p][ph] = (h[2p - a_ph], h[2p + 1 - a_ph])
   int32_t tsub, np, L, M, K, S;  // what the tables were built for (checked at launch)
+  // The DF2 realisation (cascade.h, NORM form): per stage {c1, c2, a1, a2}
+  // and the input gain.  Read through the scalar cache right where pass 2
+  // needs them instead of occupying ~50 SGPRs as kernel arguments for the
+  // whole kernel (which made the compiler spill SGPRs to VGPR lanes).
+  double cf[kS][4];
+  double gain;
 };
 
 struct TileArgs {
@@ -146,7 +152,6 @@ struct TileArgs {
   const float* taps;        // device taps [K]
   int64_t c;                // 'same' offset of the expanded convolution
   int K, L, M, T, win;      // win: floats of one wave's x window
-  SosParams p;
 };
 
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
@@ -218,9 +223,13 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
   for (int i = 0; i < NH; ++i) acc[i] = f32x2{0.f, 0.f};
 #pragma unroll
   for (int p = 0; p < GEO::NP; ++p) {
+    // Load each pair's taps right before its FMAs (an opaque table pointer per
+    // pair keeps the compiler from hoisting all 126 tap SGPRs of a part).
+    tt_ptr tq = tt;
+    asm volatile("" : "+s"(tq));
     f32x2 t[GEO::L];
 #pragma unroll
-    for (int ph = 0; ph < GEO::L; ++ph) t[ph] = f32x2{tt->TP[p][ph][0], tt->TP[p][ph][1]};
+    for (int ph = 0; ph < GEO::L; ++ph) t[ph] = f32x2{tq->TP[p][ph][0], tq->TP[p][ph][1]};
 #pragma unroll
     for (int i = 0; i < NH; ++i)
       acc[i] = __builtin_elementwise_fma(t[GEO::phi(H0 + i)],
@@ -317,6 +326,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     for (int k = 0; k < kS; ++k)
       mac2(mt->Dp[0][k], m_in[2 * k], m_in[2 * k + 1], v[2 * k], v[2 * k + 1]);
   }
+  // m_in waits out the scan in LDS (free until the y store), not in 24 VGPRs
+  // of every lane at the kernel's register peak.
+  double* park = reinterpret_cast<double*>(lds);
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+  }
+  fence();
 #pragma unroll
   for (int lv = 0; lv < 6; ++lv) {
     const int off = 1 << lv;
@@ -331,10 +348,13 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // Entry state of the lane's sub-chunk: v of the lane before (m_in for lane 0).
   double m[kD];
 #pragma unroll
-  for (int d = 0; d < kD; ++d) {
-    const double t = shfl_up_f64(v[d], 1);
-    m[d] = lane == 0 ? m_in[d] : t;
+  for (int d = 0; d < kD; ++d) m[d] = shfl_up_f64(v[d], 1);
+  fence();
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kD; ++d) m[d] = park[d];
   }
+  fence();
 
   // ---- 4. publish the tile's end state (lane 63) for the next tile
   if (tile + 1 < a.ntiles && lane == kWave - 1) {
@@ -374,10 +394,10 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       for (int k = kS - 1; k >= 0; --k) {
         const int t = st - k;
         if (t < 0 || t >= TS) continue;
-        const double u = k == 0 ? (double)y[t] * a.p.G : pend[k - 1];
-        const double* cf = a.p.c[k];
-        const double w = fma(-cf[4], s2[k], fma(-cf[3], s1[k], u));
-        const double v2 = fma(cf[2], s2[k], fma(cf[1], s1[k], w));
+        const double u = k == 0 ? (double)y[t] * mt->gain : pend[k - 1];
+        const double c1 = mt->cf[k][0], c2 = mt->cf[k][1], a1 = mt->cf[k][2], a2 = mt->cf[k][3];
+        const double w = fma(-a2, s2[k], fma(-a1, s1[k], u));
+        const double v2 = fma(c2, s2[k], fma(c1, s1[k], w));
         s2[k] = s1[k];
         s1[k] = w;
         if (k == kS - 1) y[t] = clip_f32((float)v2, lo, hi);
@@ -840,6 +860,14 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
   if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);  // kind 2 reads the device taps
+  for (int k = 0; k < kS; ++k) {
+    // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
+    tt->cf[k][0] = p.c[k][1];
+    tt->cf[k][1] = p.c[k][2];
+    tt->cf[k][2] = p.c[k][3];
+    tt->cf[k][3] = p.c[k][4];
+  }
+  tt->gain = p.G;
   tt->tsub = (int32_t)tp.tsub;
   tt->np = tp.kind == 1 ? Geo3241::NP : 0;
   tt->L = L;
@@ -892,7 +920,6 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.M = M;
   a.T = (K + L - 1) / L;
   a.win = tp.win;
-  a.p = p;
   if (tp.kind == 1) {
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,

@@ -182,7 +182,7 @@ def test_chain_tile_tables_host_only():
     plan = design.src_plan(48000, 48000, 2, 3)
     sos = np.ascontiguousarray(design.eq_plan(72000, gains).sos)
     nbytes = lib.dsp_chain_tile_tables_bytes()
-    assert nbytes == 64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4
+    assert nbytes == 64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4 + 6 * 4 * 8 + 8
     buf = np.zeros(nbytes, np.uint8)
     taps32 = np.ascontiguousarray(plan.taps, dtype=np.float32)
     rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, 72000, taps32.ctypes.data,
@@ -192,7 +192,12 @@ def test_chain_tile_tables_host_only():
     Dp = buf[6144:7296].view(np.float64).reshape(6, 6, 2, 2)
     T = buf[7296:8448].view(np.float64).reshape(12, 12)
     TP = buf[8448:9472].view(np.float32).reshape(32, 4, 2)
-    assert tuple(buf[9472:].view(np.int32)) == (48, 21, 3, 2, 121, 6)
+    assert tuple(buf[9472:9496].view(np.int32)) == (48, 21, 3, 2, 121, 6)
+    # the DF2 realisation pass 2 reads: per stage {b1/b0, b2/b0, a1, a2}, gain prod(b0)
+    rows, gain, norm = design.df2_realization(sos)
+    assert norm
+    np.testing.assert_array_equal(buf[9496:9688].view(np.float64).reshape(6, 4), rows[:, 1:])
+    assert buf[9688:9696].view(np.float64)[0] == gain
     A, B = design.state_space(sos)
     Ti = np.linalg.inv(T)
     for d in range(6):
@@ -222,7 +227,7 @@ def test_chain_tile_tables_host_only():
     buf[:] = 0
     assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c5.n_out, t5.ctypes.data,
                                      c5.K, 160, 147, c5.c_offset, _lib.sos_pointer(sos5), 6) == 0
-    assert tuple(buf[9472:].view(np.int32)) == (32, 0, 160, 147, 1023, 6)
+    assert tuple(buf[9472:9496].view(np.int32)) == (32, 0, 160, 147, 1023, 6)
     G5 = buf[:6144].view(np.float64).reshape(64, 12)
     T5 = buf[7296:8448].view(np.float64).reshape(12, 12)
     A5, B5 = design.state_space(sos5)
