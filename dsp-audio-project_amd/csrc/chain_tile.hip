@@ -122,6 +122,14 @@ constexpr int branch_parity(int ph) {
   return a;
 }
 
+// Generic kernel geometry (k_chain_gen, below).
+constexpr int kGenTS = 32;                    // outputs per lane
+constexpr int kGenTile = kWave * kGenTS;      // outputs per tile (wave)
+constexpr int kGenWaves = 4;                  // waves (channels) per workgroup
+constexpr int kGenTT = 8;                     // taps per output row (T <= 8)
+constexpr int kGenClasses = 8;                // max sub-chunk phase classes
+constexpr int kGenClassStride = kGenTS * kGenTT + 4;  // LDS floats per class (+4: bank spread)
+
 // Tables of the single-pass kernel, built on the host in float64
 // (dsp_chain_tile_tables) and read by the kernel through the scalar cache.
 struct TileTables {
@@ -136,6 +144,14 @@ struct TileTables {
   // whole kernel (which made the compiler spill SGPRs to VGPR lanes).
   double cf[kS][4];
   double gain;
+  // Generic kernel: sub-chunks start at outputs m = 32 j, whose polyphase
+  // branch (32 j M + c) mod L takes `classes` values (class of j: j mod
+  // classes).  seq[k][i] = the taps of output i of a class-k sub-chunk (u < T,
+  // zero beyond); bit i of adv[k] = 1 when q advances by M div L + 1 (not
+  // M div L) from output i to i + 1.
+  float seq[kGenClasses][kGenTS][kGenTT];
+  uint32_t adv[kGenClasses];
+  int32_t classes, pad;
 };
 
 struct TileArgs {
@@ -460,64 +476,56 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 
 // ---------------------------------------------------------------------------
 // Generic single-pass kernel: any L, M with ceil(K/L) <= 8 (config 5's
-// L/M = 160/147, K = 1023: 7 taps per branch).  The polyphase branch of a
-// lane's outputs changes from output to output and from lane to lane, so the
-// SRC reads its taps and samples from LDS at run-time offsets instead of the
-// specialised kernel's wave-uniform scalar taps:
-//   j = m*M + c, phi = j mod L, q = j div L (incremental per output),
+// L/M = 160/147, K = 1023: 7 taps per branch) and at most 8 phase classes.
+// The polyphase branch of a lane's outputs changes from output to output and
+// from lane to lane:
+//   j = m*M + c, phi = j mod L, q = j div L,
 //   y[m] = sum_u h[phi][u] x[q - (T-1) + u],  h[phi][u] = taps[phi + L(T-1-u)],
-// summed as k_src_generic does (even u into a0, odd u into a1, y = a0 + a1),
-// so y is bitwise that kernel's.  A workgroup is kGenWaves waves, one channel
-// each at the same tile index (ids stay tile-major for the hand-off); they
-// share the tap bank [L][8] in LDS.  Each wave owns its x window (and stages
-// its stores through it).  Steps 2-5 are tile_cascade<32>.
+// summed as k_src_generic does (even u and odd u in two chains, y = even +
+// odd), so y is bitwise that kernel's.  Sub-chunks start at outputs m = 32 j,
+// and their branch sequences repeat with j mod C, C = L / gcd(32 M mod L, L)
+// (5 for 160/147): the host tabulates every class's 32 rows of taps and its
+// q-advance bits (TileTables::seq/adv), so a lane's taps for output i sit at a
+// compile-time offset of its class row and the SRC does no phase arithmetic.
+// A workgroup is kGenWaves waves, one channel each at the same tile index
+// (ids stay tile-major for the hand-off); they share the class tables in LDS.
+// Each wave owns its x window (and stages its stores through it).  Steps 2-5
+// are tile_cascade<32>.
 // ---------------------------------------------------------------------------
-constexpr int kGenTS = 32;                    // outputs per lane
-constexpr int kGenTile = kWave * kGenTS;      // outputs per tile (wave)
-constexpr int kGenWaves = 4;                  // waves (channels) per workgroup
-constexpr int kGenTT = 8;                     // bank row: taps per branch (T <= 8)
-
-// Row phi of the tap bank: 8 floats, plus 4 floats of padding after every 32
-// rows, so that the branches lanes read together (phases 32 apart for config
-// 5: (32 l M + c) mod L with 32 M = 64 mod 160) start on distinct bank quads.
-__host__ __device__ constexpr int bank_row(int phi) { return phi * kGenTT + 4 * (phi >> 5); }
-__host__ __device__ constexpr int bank_floats(int L) { return bank_row(L) + 4; }
-
 template <bool UP>
 __global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
 k_chain_gen(TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* bank = smem;  // [L][kGenTT], rows at bank_row(phi)
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
   const int64_t tile = blockIdx.x / groups;
   const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
   const int L = a.L, M = a.M, T = a.T;
-  // Tap bank, 8 loads in flight per thread per round (a loop with one load per
-  // iteration would wait out one memory latency per element).
-  constexpr int kNT = kWave * kGenWaves;
-  for (int i0 = 0; i0 < L * kGenTT; i0 += 8 * kNT) {
-    float t[8];
+  const tt_ptr mt = (tt_ptr)a.tt;
+  const int C = mt->classes;
+  // Class tables into LDS (class stride kGenClassStride floats: the rows that
+  // lanes of different classes read together start on distinct bank quads),
+  // then the advance masks; two float4 loads in flight per thread.
+  float* seq = smem;
+  uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
+  {
+    constexpr int kNT = kWave * kGenWaves;
+    constexpr int kF4 = kGenTS * kGenTT / 4;  // float4s per class
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.tt->seq);
+    f32x4 v[2];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = i0 + r * kNT + (int)threadIdx.x;
-      const int phi = i / kGenTT, u = i - phi * kGenTT;
-      const int k = phi + L * (T - 1 - u);
-      const float v = a.taps[k < 0 ? 0 : (k < a.K ? k : a.K - 1)];  // unconditional load
-      t[r] = (i < L * kGenTT && u < T && k < a.K) ? v : 0.f;
-    }
+    for (int r = 0; r < 2; ++r) v[r] = src[(r * kNT + threadIdx.x) & (kGenClasses * kF4 - 1)];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = i0 + r * kNT + (int)threadIdx.x;
-      const int phi = i / kGenTT, u = i - phi * kGenTT;
-      if (i < L * kGenTT) bank[bank_row(phi) + u] = t[r];
+    for (int r = 0; r < 2; ++r) {
+      const int i = r * kNT + threadIdx.x, k = i / kF4, f = i - k * kF4;
+      if (k < C) *reinterpret_cast<f32x4*>(seq + k * kGenClassStride + 4 * f) = v[r];
     }
+    if (threadIdx.x < kGenClasses) adv[threadIdx.x] = a.tt->adv[threadIdx.x];
   }
   __syncthreads();
   if (b >= a.B) return;
-  const tt_ptr mt = (tt_ptr)a.tt;
-  float* win = smem + bank_floats(L) + w * a.win;
+  float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
   const int64_t m0 = tile * kGenTile;
 
   // ---- x window of the tile: x[qa .. qa + nload) (zeros outside [0, n_in))
@@ -553,29 +561,27 @@ k_chain_gen(TileArgs a) {
   {
     const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
     const int64_t q0 = j0 / L;
-    int phi = (int)(j0 - q0 * L);
     int qr = (int)(q0 - (T - 1) - qa);  // window offset of the output's first tap
-    const int dq = M / L, dphi = M - dq * L;
+    const int dq = M / L;
+    const int cls = (int)((tile * kWave + lane) % C);  // sub-chunk j = m0/32 + lane
+    const float* row = seq + cls * kGenClassStride;   // output i's taps at row + 8 i
+    const uint32_t am = adv[cls];
     float w[kGenTT];
 #pragma unroll
     for (int u = 0; u < kGenTT; ++u) w[u] = win[qr + u];
-    const float* hr = bank + bank_row(phi);
-    float4 h0 = *reinterpret_cast<const float4*>(hr);
-    float4 h1 = *reinterpret_cast<const float4*>(hr + 4);
+    float4 h0 = *reinterpret_cast<const float4*>(row);
+    float4 h1 = *reinterpret_cast<const float4*>(row + 4);
     float nx = UP ? win[qr + kGenTT] : 0.f;  // enters the window if q advances
 #pragma unroll
     for (int i = 0; i < kGenTS; ++i) {
-      // indices and operands of output i+1
-      int phi_n = phi + dphi, qr_n = qr + dq;
-      const bool carry = phi_n >= L;
-      phi_n = carry ? phi_n - L : phi_n;
-      qr_n = carry ? qr_n + 1 : qr_n;
+      // operands of output i+1
+      const bool carry = (am >> i) & 1u;
+      const int qr_n = qr + dq + (carry ? 1 : 0);
       float4 h0n, h1n;
       float nxn = 0.f, wn[kGenTT];
       if (i + 1 < kGenTS) {
-        const float* hrn = bank + bank_row(phi_n);
-        h0n = *reinterpret_cast<const float4*>(hrn);
-        h1n = *reinterpret_cast<const float4*>(hrn + 4);
+        h0n = *reinterpret_cast<const float4*>(row + kGenTT * (i + 1));
+        h1n = *reinterpret_cast<const float4*>(row + kGenTT * (i + 1) + 4);
         if constexpr (UP) {
           nxn = win[qr_n + kGenTT];
         } else {
@@ -603,7 +609,6 @@ k_chain_gen(TileArgs a) {
         }
         h0 = h0n;
         h1 = h1n;
-        phi = phi_n;
         qr = qr_n;
       }
     }
@@ -631,8 +636,24 @@ int gen_window(int L, int M, int T) {
   return (int)std::max<int64_t>(r, staging_floats(kGenTS));
 }
 
-size_t gen_lds_bytes(int L, int win) {
-  return ((size_t)bank_floats(L) + (size_t)kGenWaves * win) * sizeof(float);
+size_t gen_lds_bytes(int win) {
+  return ((size_t)kGenClasses * kGenClassStride + kGenClasses + (size_t)kGenWaves * win) *
+         sizeof(float);
+}
+
+int64_t gcd64(int64_t a, int64_t b) {
+  while (b) {
+    const int64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// Phase classes of the generic kernel's sub-chunk starts (outputs 32 j):
+// L / gcd(32 M mod L, L).
+int gen_classes(int L, int M) {
+  return (int)(L / gcd64(((int64_t)kGenTS * M) % L, L));
 }
 constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
 
@@ -653,9 +674,9 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
     tp->win = 0;
     return true;
   }
-  if (TT <= kGenTT && L <= 4096) {
+  if (TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
     const int win = gen_window(L, M, TT);
-    if (gen_lds_bytes(L, win) <= kGenLdsMax) {
+    if (gen_lds_bytes(win) <= kGenLdsMax) {
       tp->kind = 2;
       tp->tsub = kGenTS;
       tp->tile = kGenTile;
@@ -817,6 +838,26 @@ void tap_pairs(const float* taps, int K, TileTables* tt) {
       }
 }
 
+// Class tables of the generic kernel (TileTables::seq / adv).
+void gen_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables* tt) {
+  const int T = (K + L - 1) / L, C = gen_classes(L, M);
+  const int64_t step = ((int64_t)kGenTS * M) % L, dphi = M % L;
+  for (int k = 0; k < C; ++k) {
+    int64_t phi = (c % L + k * step) % L;  // branch of the class's first output
+    uint32_t bits = 0;
+    for (int i = 0; i < kGenTS; ++i) {
+      for (int u = 0; u < kGenTT; ++u) {
+        const int64_t idx = phi + (int64_t)L * (T - 1 - u);
+        tt->seq[k][i][u] = (u < T && idx < K) ? taps[idx] : 0.f;
+      }
+      if (phi + dphi >= L) bits |= 1u << i;
+      phi = (phi + dphi) % L;
+    }
+    tt->adv[k] = bits;
+  }
+  tt->classes = C;
+}
+
 struct TileWs {
   size_t err_off, st_off, fl_off, total;
 };
@@ -859,7 +900,8 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   TileTables* tt = static_cast<TileTables*>(out);
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
-  if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);  // kind 2 reads the device taps
+  if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);
+  else gen_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
     tt->cf[k][0] = p.c[k][1];
@@ -928,7 +970,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     DSP_REQUIRE(taps, "null taps");
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
-    const size_t shm = gen_lds_bytes(L, tp.win);
+    const size_t shm = gen_lds_bytes(tp.win);
     auto kern = M < L ? k_chain_gen<true> : k_chain_gen<false>;
     if (int rc = allow_lds(kern, shm)) return rc;
     TraceScope trace("chain_tile", s);

@@ -182,7 +182,8 @@ def test_chain_tile_tables_host_only():
     plan = design.src_plan(48000, 48000, 2, 3)
     sos = np.ascontiguousarray(design.eq_plan(72000, gains).sos)
     nbytes = lib.dsp_chain_tile_tables_bytes()
-    assert nbytes == 64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4 + 6 * 4 * 8 + 8
+    assert nbytes == (64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4 + 6 * 4 * 8 + 8
+                      + 8 * 32 * 8 * 4 + 8 * 4 + 2 * 4)
     buf = np.zeros(nbytes, np.uint8)
     taps32 = np.ascontiguousarray(plan.taps, dtype=np.float32)
     rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, 72000, taps32.ctypes.data,
@@ -237,6 +238,19 @@ def test_chain_tile_tables_host_only():
         X = A5 @ X + B5 * v
     np.testing.assert_allclose(T5 @ (G5[:32].T @ y), X, rtol=1e-10, atol=1e-12)
     assert not buf[8448:9472].any()
+    # class tables: sub-chunks start at outputs 32 j; class j mod 5 (32*147 mod 160 = 64)
+    seq = buf[9696:9696 + 8192].view(np.float32).reshape(8, 32, 8)
+    adv = buf[17888:17920].view(np.uint32)
+    assert tuple(buf[17920:17928].view(np.int32))[0] == 5
+    L, M, K, c = 160, 147, 1023, c5.c_offset
+    for k in range(5):
+        phi = (c + k * 64) % L
+        for i in range(32):
+            want = [t5[phi + L * (6 - u)] if u < 7 and phi + L * (6 - u) < K else 0.0
+                    for u in range(8)]
+            np.testing.assert_array_equal(seq[k, i], np.array(want, dtype=np.float32))
+            assert ((int(adv[k]) >> i) & 1) == int(phi + M >= L)
+            phi = (phi + M) % L
     c6 = design.src_plan(48000, 44100, 147, 160)
     t6 = np.ascontiguousarray(c6.taps, dtype=np.float32)
     assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c6.n_out, t6.ctypes.data,
