@@ -165,8 +165,10 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
  *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
  *       with wave-uniform taps: configs 3 and 4), or
- *   32: any other L/M with ceil(K/L) <= 8 whose tap bank and four x windows
- *       fit 64 KB of LDS (run-time taps: config 5's 160/147, K = 1023),
+ *   32: any other L/M with ceil(K/L) <= 8, at most 8 branch classes of the
+ *       32-output sub-chunk starts (L / gcd(32 M mod L, L)) and four x windows
+ *       that fit 64 KB of LDS with the class tables (config 5's 160/147,
+ *       K = 1023: 5 classes),
  * `tile_tables` is a device copy (256-byte aligned) of the tables
  * dsp_chain_tile_tables built for this call's geometry, taps and sos, and the
  * rows of x, y and z are 16-byte aligned with pitches that are multiples of 4
