@@ -199,8 +199,9 @@ def valu_work(chain, mean_ms):
 
 def load_traffic(wl_name, channels):
     """PMC HBM bytes per launch for this workload and batch, from the summary
-    tools/pmc_parse.py --write keeps in profiles/pmc_traffic.json."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    tools/pmc_parse.py --write keeps in pmc_traffic.json (repo root: profiles/ is
+    not sent to the GPU box)."""
+    path = os.path.join(ROOT, "pmc_traffic.json")  # profiles/ does not travel to the GPU box
     try:
         with open(path) as f:
             ent = json.load(f).get(wl_name, {})

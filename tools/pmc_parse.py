@@ -4,7 +4,7 @@ HBM traffic per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly hal
 the bytes of a 16-B-per-lane coalesced stream on gfx950, so
     traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes.
 With --write WORKLOAD CHANNELS SOURCE it records the per-launch traffic in
-profiles/pmc_traffic.json under the bench workload name (config3, config4,
+pmc_traffic.json (repo root) under the bench workload name (config3, config4,
 config5) for that batch; bench.py reports it as roofline.traffic when its own
 batch matches."""
 import csv
@@ -62,7 +62,7 @@ def main(root, write=None):
             print(f"   traffic (2*FETCH+WRITE)     {t / 1e9:.4f} GB per launch")
     if write:
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                            "profiles", "pmc_traffic.json")
+                            "pmc_traffic.json")
         data = {}
         if os.path.exists(path):
             with open(path) as fh:
