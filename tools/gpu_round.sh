@@ -1,0 +1,33 @@
+# Round measurement: GPU parity tests, smoke, bench lines (config 4 default and
+# config 5), rocprofv3 kernel stats of the same bench commands, PMC passes
+# (HBM traffic + SQ counters) for both -> gpurun_out/$TAG/.
+#   bash tools/gpu_round.sh TAG
+set -o pipefail
+TAG=${1:-round}
+cd "$GRAFT_REPO_ROOT"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/$TAG"
+rm -rf "$OUT"; mkdir -p "$OUT"
+echo "== pytest gpu"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; tail -2 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
+echo "== smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+for c in c4 c5; do
+  echo "== bench $c"
+  timeout -k 10 600 python bench.py --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
+  cut -c1-300 "$OUT/bench_$c.json"
+done
+cd /tmp && export TMPDIR=/tmp
+for c in c4 c5; do
+  echo "== rocprof stats $c"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config $c --steps 20 --warmup 5 --cpu-per-proc 0 --no-config3 > "$OUT/prof_$c.log" 2>&1 || { tail -20 "$OUT/prof_$c.log"; exit 1; }
+  find "$OUT/prof_$c" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$c.csv" \;
+  cut -d, -f1-4 "$OUT/kernel_stats_$c.csv" | head -4 | cut -c1-200
+  grep '^{' "$OUT/prof_$c.log" | cut -c1-200
+done
+cd "$GRAFT_REPO_ROOT"
+bash tools/pmc_chain.sh "$TAG/pmc_c4" 3 c4 > "$OUT/pmc_c4.log" 2>&1 || { tail -20 "$OUT/pmc_c4.log"; exit 1; }
+bash tools/pmc_chain.sh "$TAG/pmc_c5" 3 c5 > "$OUT/pmc_c5.log" 2>&1 || { tail -20 "$OUT/pmc_c5.log"; exit 1; }
+grep -E "^==|traffic" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c4/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c5/pmc_summary.txt"
+echo done
