@@ -80,10 +80,22 @@ def rank_channels(total: int, rank: int, world: int) -> tuple[int, int]:
     return ranges[rank] if rank < len(ranges) else (total, total)
 
 
-def timed_loop(step, steps, warmup, sync, dist=None):
-    """W untimed steps, then K steps bracketed by barrier + sync on both sides.
+PREHEAT_S = 0.3   # untimed steps before the warmup: GPU clocks settle
+
+
+def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
+    """Untimed steps for PREHEAT_S seconds (the MI355X boosts, then throttles,
+    then settles over the first ~20-40 ms of a busy GPU: a 1 ms config-3 step
+    measured 0.86 -> 1.19 -> 0.89 ms over its first 20 launches), then W untimed
+    warmup steps, then K steps bracketed by barrier + sync on both sides.
     Returns the elapsed seconds, maxed over ranks when `dist` is initialised
     (a gloo group: the max is a CPU all-reduce)."""
+    t_pre = time.perf_counter()
+    while preheat_s > 0:
+        step()
+        sync()
+        if time.perf_counter() - t_pre >= preheat_s:
+            break
     for _ in range(warmup):
         step()
     sync()
@@ -362,6 +374,7 @@ def main(argv=None):
                 "L": wl["L"], "M": wl["M"], "n_fft": wl["n_fft"],
                 "parallelism": f"channel-shard x{world} (no collective)",
                 "launch": launch,
+                "preheat_s": PREHEAT_S,
             },
             "roofline": {
                 "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),

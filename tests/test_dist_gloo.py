@@ -33,7 +33,8 @@ def _worker(rank, world, port, out):
             calls.append(1)
             time.sleep(delay)
 
-        elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, dist=dist)
+        elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, dist=dist,
+                                   preheat_s=0)
         lo, hi = shard_ranges(32768, world)[rank]
         assert bench.rank_channels(bench.WORKLOADS["c4"]["channels"], rank, world) == (lo, hi)
         out[rank] = (elapsed, len(calls), lo, hi)
@@ -52,3 +53,20 @@ def test_two_rank_timing_is_max_over_ranks():
     assert e0 == pytest.approx(e1)             # both report the max over ranks
     assert e0 >= 3 * 0.04 * 0.95               # ... which is the slow rank's time
     assert (lo0, hi0, lo1, hi1) == (0, 16384, 16384, 32768)
+
+
+def test_timed_loop_preheat_then_exact_counts():
+    """bench.timed_loop runs untimed steps for preheat_s seconds, then exactly
+    W warmup and K timed steps (the timed region covers only the K)."""
+    import time as _t
+
+    import bench
+    calls = []
+
+    def step():
+        calls.append(_t.perf_counter())
+        _t.sleep(0.002)
+
+    elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, preheat_s=0.03)
+    assert len(calls) >= 2 + 3 + 10          # >= 30 ms of 2 ms pre-heat steps
+    assert 0.005 <= elapsed < 0.05           # only the 3 timed steps
