@@ -326,9 +326,15 @@ struct RealSpecIO {
   InRow ir;
   float2* buf;
   bool live;
+  bool pairs;  // the frame's samples start 8-byte aligned: one float2 load per pair
   __device__ __forceinline__ float2 load(int n) const {
     if (!live) return make_float2(0.f, 0.f);
     const int i = 2 * n;
+    if (pairs && i + 1 < ir.valid) {
+      const float2 sv = *reinterpret_cast<const float2*>(a.in + ir.base + i);
+      const float2 wv = reinterpret_cast<const float2*>(a.win)[n];
+      return make_float2(sv.x * wv.x, sv.y * wv.y);
+    }
     const float s0 = (i < ir.valid) ? a.in[ir.base + i] : 0.f;
     const float s1 = (i + 1 < ir.valid) ? a.in[ir.base + i + 1] : 0.f;
     return make_float2(s0 * a.win[i], s1 * a.win[i + 1]);
@@ -348,8 +354,10 @@ __global__ __launch_bounds__(Plan<LOG2N - 1>::NT) void k_spec_real(FftArgs a) {
   float2* buf = lds + tl * PL::PADN;
   Tw<LOG2N - 1, 0> tw;
   load_tw<LOG2N - 1, 0>(tw, a.tw, j0, 2);
-  run_pass<LOG2N - 1, 0>(RealSpecIO<NH>{a, in_row<kSpec>(a, live ? t : 0), buf, live}, buf, j0,
-                         tw);
+  const InRow ir = in_row<kSpec>(a, live ? t : 0);
+  const bool pairs = ((reinterpret_cast<uintptr_t>(a.in + ir.base) & 7) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(a.win) & 7) == 0);
+  run_pass<LOG2N - 1, 0>(RealSpecIO<NH>{a, ir, buf, live, pairs}, buf, j0, tw);
   __syncthreads();  // the last pass stored Z into LDS
   if (!live) return;
   float* mr = a.out + t * a.ld_out;
