@@ -159,17 +159,29 @@ unsigned io_blocks(int64_t n) {
   return (unsigned)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
 }
 
+// Rows ride on the grid's y extent (<= 65535): larger batches launch in
+// consecutive row ranges, f(b0, nb) once per range.
+constexpr int64_t kMaxRowsY = 65535;
+template <class F>
+int for_row_ranges(int64_t B, F f) {
+  for (int64_t b0 = 0; b0 < B; b0 += kMaxRowsY)
+    if (int rc = f(b0, B - b0 < kMaxRowsY ? B - b0 : kMaxRowsY)) return rc;
+  return DSP_OK;
+}
+
 int absmax(const float* x, int64_t B, int64_t n, int64_t ld, uint32_t* peak, bool nan0,
            hipStream_t s) {
   DSP_HIP(hipMemsetAsync(peak, 0, (size_t)B * sizeof(uint32_t), s));
   if (n == 0) return DSP_OK;
-  const dim3 grid(io_blocks(n), (unsigned)B);
-  if (nan0)
-    hipLaunchKernelGGL(k_absmax<true>, grid, dim3(kIoNT), 0, s, x, n, ld, peak);
-  else
-    hipLaunchKernelGGL(k_absmax<false>, grid, dim3(kIoNT), 0, s, x, n, ld, peak);
-  DSP_LAUNCHED("k_absmax");
-  return DSP_OK;
+  return for_row_ranges(B, [&](int64_t b0, int64_t nb) {
+    const dim3 grid(io_blocks(n), (unsigned)nb);
+    if (nan0)
+      hipLaunchKernelGGL(k_absmax<true>, grid, dim3(kIoNT), 0, s, x + b0 * ld, n, ld, peak + b0);
+    else
+      hipLaunchKernelGGL(k_absmax<false>, grid, dim3(kIoNT), 0, s, x + b0 * ld, n, ld, peak + b0);
+    DSP_LAUNCHED("k_absmax");
+    return DSP_OK;
+  });
 }
 
 uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
@@ -255,13 +267,15 @@ int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t
   if (B == 0 || frames == 0) return DSP_OK;
   DSP_REQUIRE(pcm && out, "null pointer");
   const uint8_t* p = static_cast<const uint8_t*>(pcm);
-  const dim3 grid(io_blocks(frames), (unsigned)B);
 #define DSP_PCM(F, BI)                                                                        \
   if (format == F && bits == BI) {                                                            \
-    hipLaunchKernelGGL((k_pcm_mono<F, BI>), grid, dim3(kIoNT), 0, s, p, channels, frames,   \
-                       ld_bytes, out, ld_out);                                                \
-    DSP_LAUNCHED("k_pcm_mono");                                                               \
-    return DSP_OK;                                                                            \
+    return for_row_ranges(B, [&](int64_t b0, int64_t nb) {                                    \
+      hipLaunchKernelGGL((k_pcm_mono<F, BI>), dim3(io_blocks(frames), (unsigned)nb),          \
+                         dim3(kIoNT), 0, s, p + b0 * ld_bytes, channels, frames, ld_bytes,    \
+                         out + b0 * ld_out, ld_out);                                          \
+      DSP_LAUNCHED("k_pcm_mono");                                                             \
+      return DSP_OK;                                                                          \
+    });                                                                                       \
   }
   DSP_PCM(DSP_WAV_PCM, 8)
   DSP_PCM(DSP_WAV_PCM, 16)
@@ -281,10 +295,12 @@ int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double thr
   TraceScope trace("peak_normalize", s);
   if (int rc = absmax(x, B, n, ld, peak, false, s)) return rc;
   if (n == 0) return DSP_OK;
-  hipLaunchKernelGGL(k_scale, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, x, n, ld,
-                     peak, threshold);
-  DSP_LAUNCHED("k_scale");
-  return DSP_OK;
+  return for_row_ranges(B, [&](int64_t b0, int64_t nb) {
+    hipLaunchKernelGGL(k_scale, dim3(io_blocks(n), (unsigned)nb), dim3(kIoNT), 0, s, x + b0 * ld,
+                       n, ld, peak + b0, threshold);
+    DSP_LAUNCHED("k_scale");
+    return DSP_OK;
+  });
 }
 
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
@@ -296,14 +312,17 @@ int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, in
   TraceScope trace("quantize16", s);
   if (int rc = absmax(z, B, n, ld_z, peak, true, s)) return rc;
   if (n == 0) return DSP_OK;
-  if (precision == 32)
-    hipLaunchKernelGGL(k_quantize16<true>, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z,
-                       n, ld_z, out, ld_out, peak);
-  else
-    hipLaunchKernelGGL(k_quantize16<false>, dim3(io_blocks(n), (unsigned)B), dim3(kIoNT), 0, s, z,
-                       n, ld_z, out, ld_out, peak);
-  DSP_LAUNCHED("k_quantize16");
-  return DSP_OK;
+  return for_row_ranges(B, [&](int64_t b0, int64_t nb) {
+    const dim3 grid(io_blocks(n), (unsigned)nb);
+    if (precision == 32)
+      hipLaunchKernelGGL(k_quantize16<true>, grid, dim3(kIoNT), 0, s, z + b0 * ld_z, n, ld_z,
+                         out + b0 * ld_out, ld_out, peak + b0);
+    else
+      hipLaunchKernelGGL(k_quantize16<false>, grid, dim3(kIoNT), 0, s, z + b0 * ld_z, n, ld_z,
+                         out + b0 * ld_out, ld_out, peak + b0);
+    DSP_LAUNCHED("k_quantize16");
+    return DSP_OK;
+  });
 }
 
 }  // namespace dsp

@@ -117,3 +117,25 @@ def test_playback_quantization_matches_app_bitwise(gpu):
     assert wav == buf.getvalue()
     with pytest.raises(ValueError):
         audio_io.quantize_pcm16(zt, precision=16)
+
+
+@pytest.mark.gpu
+def test_batches_past_the_grid_row_limit(gpu):
+    """Batches of more than 65535 rows (the grid's y extent) run as
+    consecutive row ranges: quantize and peak-normalise every row of a
+    70000-row batch, rows on both sides of the split equal to the oracle."""
+    from dspcore import audio_io
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(70)
+    B, n = 70000, 16
+    z = (rng.uniform(-1, 1, (B, n)) * rng.uniform(0.5, 4.0, (B, 1))).astype(np.float32)
+    zt = torch.from_numpy(z).to(gpu)
+    q = audio_io.quantize_pcm16(zt).cpu().numpy()
+    for b in (0, 65534, 65535, 65536, B - 1):
+        np.testing.assert_array_equal(q[b], orc.playback_pcm16(z[b].astype(np.float64)))
+    xt = zt.clone()
+    peaks = audio_io.peak_normalize(xt).cpu().numpy()
+    np.testing.assert_array_equal(peaks, np.max(np.abs(z), axis=1))
+    x = xt.cpu().numpy()
+    for b in (0, 65535, 65536, B - 1):
+        np.testing.assert_array_equal(x[b], z[b] / np.max(np.abs(z[b])))
