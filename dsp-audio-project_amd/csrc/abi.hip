@@ -94,7 +94,7 @@ size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n) {
   return dsp::fft_workspace_bytes(B, log2n);
 }
 
-int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
+int dsp_fft_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
                        const float* twiddles, void* workspace, size_t workspace_bytes,
                        void* stream) {

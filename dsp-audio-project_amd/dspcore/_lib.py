@@ -47,7 +47,7 @@ _SIGNATURES = {
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _dp, _c_i32, _c_i32, _c_i64,
         _vp, _vp, _c_sz, _vp]),
     "dsp_fft_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
-    "dsp_fft_r2_c2c_f32": (ctypes.c_int, [
+    "dsp_fft_c2c_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "dsp_spectrum_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp,

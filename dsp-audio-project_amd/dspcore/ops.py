@@ -246,10 +246,10 @@ def fft(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     ws = _fft_workspace(B, lg, x.device)
     lib = _lib.load()
     with torch.cuda.device(x.device):
-        rc = lib.dsp_fft_r2_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), ld(x),
+        rc = lib.dsp_fft_c2c_f32(_ptr(x), _ptr(out), B, lg, int(real), ld(x),
                                     ld(out), _ptr(tw), _ptr(ws), 0 if ws is None else ws.numel(),
                                     _stream(x.device))
-    _lib.check(rc, "dsp_fft_r2_c2c_f32")
+    _lib.check(rc, "dsp_fft_c2c_f32")
     return out
 
 

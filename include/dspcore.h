@@ -89,8 +89,10 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
                            size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
- * Radix-2 decimation-in-time FFT, batched, natural-order output.
- * Replaces dsp_core.py:41-66 (fft_diezmado_en_tiempo).  N = 2^log2n,
+ * Batched complex FFT of power-of-two length, natural-order output: the DFT
+ * that dsp_core.py:41-66 (fft_diezmado_en_tiempo, a recursive radix-2 DIT)
+ * computes, here as radix-16 Stockham passes in LDS (round 1 named the entry
+ * dsp_fft_r2_c2c_f32 after the reference's radix-2).  N = 2^log2n,
  * 0 <= log2n <= DSP_MAX_LOG2N_FFT.  real_input != 0: `in` is float32
  * [B][ld_in] real samples; otherwise interleaved complex [B][ld_in] (ld in
  * complex elements).  `out` is interleaved complex [B][ld_out].  `twiddles` is
@@ -101,7 +103,7 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
  * >= dsp_fft_workspace_bytes(B, log2n) = B * N * 8 bytes; 0 below).
  * ------------------------------------------------------------------------- */
 size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n);
-int dsp_fft_r2_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
+int dsp_fft_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
                        const float* twiddles, void* workspace, size_t workspace_bytes,
                        void* stream);
@@ -129,7 +131,7 @@ int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_
  * x[seg_start : seg_start + seg_len] zero-padded to N = 2^log2n (:76-82),
  * times window[N] (Hann, :85-87), FFT (:90), |X[k]| for k <= N/2 (:91,:97-98).
  * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.  log2n <= DSP_MAX_LOG2N_FFT;
- * above DSP_MAX_LOG2N the workspace rules of dsp_fft_r2_c2c_f32 apply.
+ * above DSP_MAX_LOG2N the workspace rules of dsp_fft_c2c_f32 apply.
  * ------------------------------------------------------------------------- */
 int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
                      int64_t seg_start, int64_t seg_len, int32_t log2n,
