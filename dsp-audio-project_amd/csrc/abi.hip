@@ -61,7 +61,7 @@ void clear_error() { g_error.clear(); }
 
 extern "C" {
 
-int dsp_version(void) { return 10100; /* 1.1.0 */ }
+int dsp_version(void) { return 10200; /* 1.2.0: dsp_fft_c2c_f32, chain tables with coefficients and class rows */ }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
 

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 10100
+    assert lib.dsp_version() == 10200
     assert isinstance(_lib.last_error(), str)
 
 
