@@ -583,6 +583,40 @@ def test_chain_config4_one_gpu_and_shards(gpu):
         del sh, ys, zs, ms
 
 
+def test_chain_config5_full_batch_and_shards(gpu):
+    """Config 5 at full size on one GPU (8192 x 48000 at 44.1 kHz, L/M =
+    160/147, K = 1023: the generic single-pass kernel): spot rows against the
+    oracle on both sides of the 2-way split, and the last shard of the 2-, 4-
+    and 8-GPU splits (4096 / 2048 / 1024 channels) bitwise equal to the full
+    run's rows (the kernel's arithmetic depends on L, M, K only)."""
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.shard import shard_ranges
+    from oracle import dsp_ref_cpu as orc
+    B = 8192
+    cfg = ChainConfig(48000, 44100, 160, 147, 1023, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 32
+    gen = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.rand((B, 48000), generator=gen, device=gpu) * 2 - 1
+    y, z, mag = ch.run(x)
+    torch.cuda.synchronize()
+    assert ch.handoff_ok()
+    assert float(z.abs().max()) <= 1.0 and torch.isfinite(mag).all()
+    for b in (0, 4095, 4096, B - 1):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 44100, 160, 147, orc.CONFIG3_GAINS,
+                                       1023, 4096)
+        assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL
+        assert np.max(np.abs(z[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+    for parts in (2, 4, 8):
+        lo, hi = shard_ranges(B, parts)[-1]
+        sh = Chain(cfg, hi - lo, gpu, plan_batch=B)
+        ys, zs, ms = sh.run(x[lo:hi])
+        assert torch.equal(ys, y[lo:hi]) and torch.equal(zs, z[lo:hi]) and torch.equal(ms, mag[lo:hi])
+        assert sh.handoff_ok()
+        del sh, ys, zs, ms
+
+
 def test_shards_plan_with_the_job_batch(gpu):
     """Two-launch geometry (config 5's L/M = 160/147), 4096 rows: planned with
     the job's batch (Chain(plan_batch=4096)) every shard of 1, 2 and 4 runs the
