@@ -405,7 +405,10 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // six stage updates of a step are independent (six FMA chains in flight
   // instead of one 24-deep chain per sample).  Per sample and stage the
   // operations are cascade_step's: the results are bitwise the same.
-  const float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+  float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+  // Opaque uniform bounds: otherwise the compiler clips to +-1 and selects the
+  // unclipped value per sample (4 VALU per sample instead of max + min).
+  asm volatile("" : "+v"(lo), "+v"(hi));
   {
     double pend[kS];  // pend[k]: stage k's output from the previous step
 #pragma unroll
