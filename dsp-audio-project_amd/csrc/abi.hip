@@ -61,7 +61,7 @@ void clear_error() { g_error.clear(); }
 
 extern "C" {
 
-int dsp_version(void) { return 10200; /* 1.2.0: dsp_fft_c2c_f32, chain tables with coefficients and class rows */ }
+int dsp_version(void) { return 10300; /* 1.3.0: chain tables with the shifted class rows of k_chain_gct */ }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
 

@@ -133,6 +133,10 @@ constexpr int kGenWaves = 4;                  // waves (channels) per workgroup
 constexpr int kGenTT = 8;                     // taps per output row (T <= 8)
 constexpr int kGenClasses = 8;                // max sub-chunk phase classes
 constexpr int kGenClassStride = kGenTS * kGenTT + 4;  // LDS floats per class (+4: bank spread)
+// Select-free variant for a compile-time ratio (k_chain_gct<L, M>, below).
+constexpr int kCtTaps = 10;   // tap slots per output: T <= 8 taps shifted by 0..2
+constexpr int kCtRow = 12;    // floats per output row (b128 + b128 + b64 reads)
+constexpr int kCtClassStride = kGenTS * kCtRow + 4;  // 388: class rows on distinct bank quads
 
 // Tables of the single-pass kernel, built on the host in float64
 // (dsp_chain_tile_tables) and read by the kernel through the scalar cache.
@@ -156,6 +160,12 @@ struct TileTables {
   float seq[kGenClasses][kGenTS][kGenTT];
   uint32_t adv[kGenClasses];
   int32_t classes, pad;
+  // k_chain_gct<L, M>: the same class rows with the lane's window offset
+  // folded in.  Output i of a class-k sub-chunk reads the window pairs from
+  // (i M div L) rounded down to even; seqs[k][i][v] = h[v - s_i] with the
+  // shift s_i = (i M div L) mod 2 + (1 if the class's phase carries q one
+  // further, else 0), zero outside the T taps.
+  alignas(16) float seqs[kGenClasses][kGenTS][kCtRow];
 };
 
 struct TileArgs {
@@ -624,12 +634,104 @@ k_chain_gen(TileArgs a) {
   tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
 }
 
+// ---------------------------------------------------------------------------
+// Select-free generic kernel for a compile-time ratio M < L (config 5's
+// 160/147).  Output i of a lane reads x[q_i - (T-1) + u], q_i = q_0 + g_i +
+// d_i with g_i = i M div L (compile-time) and d_i in {0, 1} (the class's
+// phase carry).  The host folds d_i and the parity of g_i into the class rows
+// (TileTables::seqs: T taps shifted by 0..2 in 10 slots), so output i sums
+// its row against the window pairs from g_i rounded down to even -- registers
+// at compile-time indices: no window sliding, no per-lane selects.  A shift
+// of 1 swaps which half of the v_pk_fma_f32 holds the even-u and the odd-u
+// chain; the extra slots hold zero taps (x * 0 + acc == acc, and +0 stays
+// +0), so y = even + odd is bitwise k_chain_gen's and k_src_generic's.
+// ---------------------------------------------------------------------------
+template <int L, int M>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gct(TileArgs a) {
+  static_assert(M < L, "q advances by 0 or 1 per output");
+  constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
+  const int64_t tile = blockIdx.x / groups;
+  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  const int T = a.T;
+  const tt_ptr mt = (tt_ptr)a.tt;
+  const int C = mt->classes;
+  // Class rows into LDS (the C classes in use only).
+  float* seq = smem;
+  {
+    constexpr int kF4 = kGenTS * kCtRow / 4;  // float4s per class
+    const f32x4* src = reinterpret_cast<const f32x4*>(&a.tt->seqs[0][0][0]);
+    for (int i = threadIdx.x; i < C * kF4; i += kWave * kGenWaves) {
+      const int k = i / kF4, f = i - k * kF4;
+      *reinterpret_cast<f32x4*>(seq + k * kCtClassStride + 4 * f) = src[i];
+    }
+  }
+  __syncthreads();
+  if (b >= a.B) return;
+  float* win = smem + C * kCtClassStride + w * a.win;
+  const int64_t m0 = tile * kGenTile;
+
+  // ---- x window of the tile: x[qa .. qa + win) (zeros outside [0, n_in))
+  const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
+  const int64_t qa = (qlo >> 2) << 2;
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int nf = a.win >> 2;
+    for (int f0 = 0; f0 < nf; f0 += 8 * kWave) {
+      f32x4 v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kWave + lane;  // past the window: harmless reads
+        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kWave + lane;
+        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+      }
+    }
+  }
+  fence();
+
+  // ---- 1. SRC of the lane's 32 outputs from its register window
+  float y[kGenTS];
+  {
+    const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
+    const float* xl = win + (int)(j0 / L - (T - 1) - qa);
+    const float* row = seq + (int)((tile * kWave + lane) % C) * kCtClassStride;
+    f32x2 X[NPW];
+#pragma unroll
+    for (int m = 0; m < NPW; ++m) X[m] = f32x2{xl[2 * m], xl[2 * m + 1]};
+#pragma unroll
+    for (int i = 0; i < kGenTS; ++i) {
+      const int g2 = (i * M / L) / 2;
+      const f32x4 t0 = *reinterpret_cast<const f32x4*>(row + kCtRow * i);
+      const f32x4 t1 = *reinterpret_cast<const f32x4*>(row + kCtRow * i + 4);
+      const f32x2 t2 = *reinterpret_cast<const f32x2*>(row + kCtRow * i + 8);
+      f32x2 acc = {0.f, 0.f};
+      acc = __builtin_elementwise_fma(f32x2{t0.x, t0.y}, X[g2], acc);
+      acc = __builtin_elementwise_fma(f32x2{t0.z, t0.w}, X[g2 + 1], acc);
+      acc = __builtin_elementwise_fma(f32x2{t1.x, t1.y}, X[g2 + 2], acc);
+      acc = __builtin_elementwise_fma(f32x2{t1.z, t1.w}, X[g2 + 3], acc);
+      acc = __builtin_elementwise_fma(t2, X[g2 + 4], acc);
+      y[i] = acc.x + acc.y;
+    }
+  }
+  pin(y);
+  tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
+}
+
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
 typedef TileGeo<3, 2, 41, 0> Geo3241;
 
 struct TilePlan {
-  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen
+  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen, 3: k_chain_gct<160, 147>
   int64_t tsub, tile, ntiles;
   int win;   // kind 2: floats of a wave's x window
 };
@@ -664,6 +766,10 @@ int gen_classes(int L, int M) {
 }
 constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
 
+size_t ct_lds_bytes(int classes, int win) {
+  return ((size_t)classes * kCtClassStride + (size_t)kGenWaves * win) * sizeof(float);
+}
+
 bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
                    TilePlan* tp) {
   if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
@@ -680,6 +786,19 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
     tp->ntiles = ceil_div(n_out, tp->tile);
     tp->win = 0;
     return true;
+  }
+  if (L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
+    // Window pairs up to (31 M div L) rounded to even + 10 past the lane's
+    // start: at most 1 float beyond gen_window's span; +4 keeps the rounding.
+    const int win = gen_window(L, M, TT) + 4;
+    if (ct_lds_bytes(gen_classes(L, M), win) <= kGenLdsMax) {
+      tp->kind = 3;
+      tp->tsub = kGenTS;
+      tp->tile = kGenTile;
+      tp->ntiles = ceil_div(n_out, tp->tile);
+      tp->win = win;
+      return true;
+    }
   }
   if (TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
     const int win = gen_window(L, M, TT);
@@ -865,6 +984,26 @@ void gen_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables
   tt->classes = C;
 }
 
+// Shifted class rows of k_chain_gct (TileTables::seqs).
+void ct_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables* tt) {
+  const int T = (K + L - 1) / L, C = gen_classes(L, M);
+  const int64_t step = ((int64_t)kGenTS * M) % L;
+  for (int k = 0; k < C; ++k) {
+    const int64_t phi0 = (c % L + k * step) % L;  // branch of the class's first output
+    for (int i = 0; i < kGenTS; ++i) {
+      const int64_t g = (int64_t)i * M / L;
+      const int64_t d = (phi0 + (int64_t)i * M) / L - g;  // 0 or 1
+      const int64_t phi = (phi0 + (int64_t)i * M) % L;
+      const int sh = (int)((g & 1) + d);
+      for (int v = 0; v < kCtRow; ++v) {
+        const int u = v - sh;
+        const int64_t idx = phi + (int64_t)L * (T - 1 - u);
+        tt->seqs[k][i][v] = (v < kCtTaps && u >= 0 && u < T && idx < K) ? taps[idx] : 0.f;
+      }
+    }
+  }
+}
+
 struct TileWs {
   size_t err_off, st_off, fl_off, total;
 };
@@ -909,6 +1048,7 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
   if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);
   else gen_sequences(taps, K, L, M, c, tt);
+  if (tp.kind == 3) ct_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
     tt->cf[k][0] = p.c[k][1];
@@ -973,6 +1113,14 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,
                        a);
+  } else if (tp.kind == 3) {
+    const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
+    DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
+    const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
+    if (int rc = allow_lds(k_chain_gct<160, 147>, shm)) return rc;
+    TraceScope trace("chain_tile", s);
+    hipLaunchKernelGGL((k_chain_gct<160, 147>), dim3((unsigned)(groups * tp.ntiles)),
+                       dim3(kWave * kGenWaves), shm, s, a);
   } else {
     DSP_REQUIRE(taps, "null taps");
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);

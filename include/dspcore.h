@@ -170,7 +170,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   32: any other L/M with ceil(K/L) <= 8, at most 8 branch classes of the
  *       32-output sub-chunk starts (L / gcd(32 M mod L, L)) and four x windows
  *       that fit 64 KB of LDS with the class tables (config 5's 160/147,
- *       K = 1023: 5 classes),
+ *       K = 1023: 5 classes; 160/147 itself runs a compile-time-ratio
+ *       instantiation whose class rows carry the window shift),
  * `tile_tables` is a device copy (256-byte aligned) of the tables
  * dsp_chain_tile_tables built for this call's geometry, taps and sos, and the
  * rows of x, y and z are 16-byte aligned with pitches that are multiples of 4
@@ -186,8 +187,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * (>= dsp_chain_tile_tables_bytes()) with the single-pass kernel's float64
  * carry tables (the cascade in block-diagonal coordinates: the sub-chunk
  * state-response rows, the powers of the diagonal blocks, the change of basis)
- * and, for the 48-sample kernel, its packed tap pairs, from the HOST float32
- * taps (the same values as `taps`, which the 32-sample kernel reads) and sos.  Returns 0 when the single-pass kernel serves the geometry
+ * and, for the 48-sample kernel, its packed tap pairs (for the 32-sample
+ * kernel, its per-class tap rows), from the HOST float32 taps and sos.  Returns 0 when the single-pass kernel serves the geometry
  * (copy the buffer to the device once and pass it to every call), 1 when it
  * does not (the two-launch path serves it; nothing to copy), DSP_EINVAL on bad
  * arguments.  With tile_tables == NULL dsp_chain_f32 takes the two-launch path.

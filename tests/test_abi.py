@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 10200
+    assert lib.dsp_version() == 10300
     assert isinstance(_lib.last_error(), str)
 
 
@@ -183,7 +183,7 @@ def test_chain_tile_tables_host_only():
     sos = np.ascontiguousarray(design.eq_plan(72000, gains).sos)
     nbytes = lib.dsp_chain_tile_tables_bytes()
     assert nbytes == (64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4 + 6 * 4 * 8 + 8
-                      + 8 * 32 * 8 * 4 + 8 * 4 + 2 * 4)
+                      + 8 * 32 * 8 * 4 + 8 * 4 + 2 * 4 + 8 + 8 * 32 * 12 * 4)   # 8: 16-B alignment
     buf = np.zeros(nbytes, np.uint8)
     taps32 = np.ascontiguousarray(plan.taps, dtype=np.float32)
     rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, 72000, taps32.ctypes.data,
@@ -251,6 +251,21 @@ def test_chain_tile_tables_host_only():
             np.testing.assert_array_equal(seq[k, i], np.array(want, dtype=np.float32))
             assert ((int(adv[k]) >> i) & 1) == int(phi + M >= L)
             phi = (phi + M) % L
+    # k_chain_gct's rows: output i reads window pairs from (i M div L) rounded
+    # down to even; its T = 7 taps sit shifted by (i M div L) mod 2 + the
+    # class's carry d_i in 10 of 12 slots
+    seqs = buf[17936:17936 + 12288].view(np.float32).reshape(8, 32, 12)
+    for k in range(5):
+        phi0 = (c + k * 64) % L
+        for i in range(32):
+            g = i * M // L
+            d = (phi0 + i * M) // L - g
+            phi = (phi0 + i * M) % L
+            sh = (g & 1) + d
+            want = [t5[phi + L * (6 - (v - sh))] if 0 <= v - sh < 7 and v < 10
+                    and phi + L * (6 - (v - sh)) < K else 0.0 for v in range(12)]
+            np.testing.assert_array_equal(seqs[k, i], np.array(want, dtype=np.float32))
+    assert not seqs[5:].any()
     c6 = design.src_plan(48000, 44100, 147, 160)
     t6 = np.ascontiguousarray(c6.taps, dtype=np.float32)
     assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c6.n_out, t6.ctypes.data,
