@@ -17,7 +17,7 @@ from collections import defaultdict
 
 def short(name):
     """Bench-trace name of a libdspcore kernel from its demangled symbol."""
-    if "k_chain_tile" in name or "k_chain_gen" in name:
+    if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gct" in name:
         return "chain_tile"
     if "k_tile_prep" in name:
         return "chain_prep"
