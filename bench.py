@@ -5,6 +5,10 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
+`--gpus N` without a launcher (WORLD_SIZE unset) starts the N ranks itself: N
+fresh child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, created
+before this process touches any GPU; the parent only relays rank 0's line.
+
 Workload (default, BASELINE.json configs[3] = SURVEY.md §8(d) config 4):
 32768 channels x 48000 samples at 48 kHz, SRC L=3/M=2 with the default 121-tap
 sinc x Blackman FIR, the 6-band EQ with gains {+6, -4, +3, -3, +5, -6} dB at
@@ -26,11 +30,16 @@ initialised).
 Rank 0 prints one JSON line.  Besides the contract fields it carries
 `roofline` (dominant kernel: algorithmic bytes per launch / its mean duration
 from HIP events the library records around every launch on the launching
-stream, and the PMC-measured HBM bytes of that kernel when profiles hold them
+stream, against the 8 TB/s spec and against a float4 copy measured in the same
+process, and the PMC-measured HBM bytes of that kernel when profiles hold them
 for this workload), `chain_roofline` (whole-chain algorithmic bytes /
-ms_per_step) and, at N = 1, `cpu_baseline`: the repo's CPU oracle (same
-numpy/scipy calls as the reference's dsp_core.py) on a bounded channel sample
-with one process per usable host core, measured BEFORE the GPU is initialised.
+ms_per_step) and, at N = 1: `cpu_baseline` (the repo's CPU oracle -- same
+numpy/scipy calls as the reference's dsp_core.py -- on a bounded channel
+sample with one process per usable host core, measured BEFORE the GPU is
+initialised), `config3` and `config5` (the other two batched configs on one
+GPU), `host_inclusive` (numpy in, H2D, chain, D2H of y/z/|X|, numpy out) and
+`copy_ceiling`.  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
+(tests of the rank launcher and sharding on CPU).
 """
 from __future__ import annotations
 
@@ -71,6 +80,38 @@ WORKLOADS = {
 def dist_env():
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
             int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` with no launcher: starts N fresh `python bench.py` children,
+    rank r on LOCAL_RANK r, rendezvous on 127.0.0.1.  This process never
+    touches a GPU (no exec from a GPU-initialised process); rank 0 writes the
+    JSON line to the shared stdout.  A failing rank ends the others."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
 
 
 def rank_channels(total: int, rank: int, world: int) -> tuple[int, int]:
@@ -240,7 +281,7 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
     x.mul_(2).sub_(1)
     torch.cuda.synchronize(device)
 
-    step = lambda: chain.run(x)  # noqa: E731
+    step = lambda: chain.run(x, check=False)  # noqa: E731
     launch = "eager"
     if not eager:
         # One chain step (no host sync, no allocation) captured into a HIP
@@ -253,7 +294,7 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
             with torch.cuda.stream(cap):
                 chain.run(x)                      # warm the LUT caches outside capture
                 with torch.cuda.graph(graph, stream=cap):
-                    chain.run(x)
+                    chain.run(x, check=False)
             torch.cuda.current_stream(device).wait_stream(cap)
             step = graph.replay
             launch = "hipGraph"
@@ -261,16 +302,16 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
             print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
     sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
     elapsed = timed_loop(step, steps, warmup, sync, dist)
-    if not chain.handoff_ok():
-        raise RuntimeError("single-pass chain: a tile hand-off wait gave up")
+    chain.check()      # raises HandoffError if a tile hand-off wait gave up
 
     # Traced pass: HIP events around every launch, on the kernels' stream.
     _lib.trace_enable(True)
     _lib.trace_read()
     for _ in range(steps):
-        chain.run(x)
+        chain.run(x, check=False)
     recs = _lib.trace_read()
     _lib.trace_enable(False)
+    chain.check()
     per = {}
     for name, ms in recs:
         per.setdefault(name, []).append(ms)
@@ -282,7 +323,100 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
     return res
 
 
+def measure_stub(wl, B, steps):
+    """DSP_BENCH_DRYRUN=1: the shapes and bookkeeping of measure() without a
+    GPU (tests of the rank launcher and sharding; numbers are placeholders)."""
+    from types import SimpleNamespace
+
+    from dspcore import design
+    src = design.src_plan(wl["n_in"], wl["fs"], wl["M"], wl["L"], wl["num_taps"])
+    spec = design.spectrum_plan(src.n_out, wl["n_fft"])
+    per = 4 * wl["n_in"] + 8 * src.n_out + 4 * (spec.n_fft // 2 + 1)
+    chain = SimpleNamespace(B=B, n_out=src.n_out, tile_len=0, cfg=SimpleNamespace(n_in=wl["n_in"]),
+                            spec=spec, algorithmic_bytes=lambda: per * B)
+    ms = 1e-6 * B + 1e-3
+    return dict(chain=chain, elapsed=steps * ms * 1e-3, launch="dry-run",
+                kernels={"chain_tile": ms}, dom="chain_tile", dom_bytes=kernel_bytes(chain, "chain_tile"))
+
+
+def extra_line(wl, r, steps):
+    """A second workload on one GPU (config 3 / config 5 next to the default
+    config 4): throughput, whole-chain and dominant-kernel HBM fractions."""
+    ms = r["elapsed"] / steps * 1e3
+    dom_ms = r["kernels"][r["dom"]]
+    dom_gbs = r["dom_bytes"] / (dom_ms * 1e-3) / 1e9
+    return {
+        "workload": wl["desc"], "channels": r["chain"].B,
+        "value": round(r["chain"].B * wl["n_in"] / (ms * 1e-3) / 1e6, 2),
+        "unit": "Msamples/s", "ms_per_step": round(ms, 4),
+        "chain_frac": round(r["chain"].algorithmic_bytes() / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "roofline": {"kernel": r["dom"], "achieved": round(dom_gbs, 1), "unit": "GB/s",
+                     "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "mean_ms": dom_ms,
+                     "algorithmic_bytes": r["dom_bytes"]},
+        "kernels_ms": r["kernels"],
+    }
+
+
+def host_inclusive(device, channels=1024, reps=3):
+    """SURVEY.md §8(d)'s host-inclusive rate: pageable numpy x in, H2D copy,
+    the chain (config-3/4 geometry, hand-off status checked), D2H of y, z and
+    |Z|, numpy out -- what the drop-in path costs per call.  Never `value`."""
+    import numpy as np
+    import torch
+
+    from dspcore.chain import Chain, ChainConfig
+    wl = WORKLOADS["c4"]
+    cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], CONFIG3_GAINS,
+                      n_fft=wl["n_fft"])
+    chain = Chain(cfg, channels, device)
+    x = np.random.default_rng(5).uniform(-1, 1, (channels, wl["n_in"])).astype(np.float32)
+
+    def once():
+        y, z, mag = chain.run(torch.from_numpy(x).to(device))
+        return y.cpu().numpy(), z.cpu().numpy(), mag.cpu().numpy()
+
+    once()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    wall = (time.perf_counter() - t0) / reps
+    moved = x.nbytes + 2 * 4 * channels * chain.n_out + 4 * channels * (wl["n_fft"] // 2 + 1)
+    del chain
+    torch.cuda.empty_cache()
+    return {"value": round(channels * wl["n_in"] / wall / 1e6, 2), "unit": "Msamples/s",
+            "channels": channels, "ms_per_call": round(wall * 1e3, 3),
+            "pcie_bytes_per_call": moved,
+            "how": "pageable numpy x -> H2D -> dsp_chain_f32 (config-4 geometry) -> D2H y, z, |Z| "
+                   "-> numpy, per call, status checked; median-free mean of 3 calls after 1 warm"}
+
+
+def copy_ceiling(device, nbytes=1 << 30, reps=20):
+    """Measured HBM ceiling in the same process: a contiguous float32 copy of
+    1 GiB (torch's vectorized copy kernel: 16-byte loads/stores), read + write
+    bytes / time."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=device).uniform_()
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return {"value": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "unit": "GB/s",
+            "how": f"torch contiguous float32 copy_ of {nbytes >> 20} MiB (read + write), "
+                   f"mean of {reps} after 3 warm, CUDA events"}
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -292,13 +426,19 @@ def main(argv=None):
                     help="total channels over all ranks (default: the config's)")
     ap.add_argument("--cpu-per-proc", type=int, default=None,
                     help="CPU-baseline channels per process (0 = skip; default per config)")
-    ap.add_argument("--no-config3", action="store_true",
-                    help="skip the extra config-3 measurement at N = 1")
+    ap.add_argument("--no-extras", "--no-config3", dest="no_extras", action="store_true",
+                    help="skip the config-3/config-5, host-inclusive and copy-ceiling "
+                         "measurements at N = 1")
     ap.add_argument("--eager", action="store_true",
                     help="launch every step from Python instead of replaying a HIP graph")
     args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))
     rank, local_rank, world = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    dry = os.environ.get("DSP_BENCH_DRYRUN") == "1"
     wl = dict(WORKLOADS[args.config])
     if args.channels:
         wl["channels"] = args.channels
@@ -309,7 +449,7 @@ def main(argv=None):
     # CPU baseline first: no GPU context exists yet when the pool forks.
     cpu = None
     per_proc = wl["cpu_per_proc"] if args.cpu_per_proc is None else args.cpu_per_proc
-    if rank == 0 and world == 1 and per_proc > 0:
+    if rank == 0 and world == 1 and per_proc > 0 and not dry:
         cpu = cpu_baseline(wl, usable_cores()[0], per_proc)
 
     import torch
@@ -319,14 +459,23 @@ def main(argv=None):
         import torch.distributed as tdist
         tdist.init_process_group("gloo")      # timing barrier + max only: no RCCL
         dist = tdist
-    # DSP_BENCH_DEVICE pins every rank to one device: a rehearsal of the
-    # multi-rank path on a one-GPU box (the driver's runs leave it unset).
-    dev_index = int(os.environ.get("DSP_BENCH_DEVICE", local_rank))
-    device = torch.device("cuda", dev_index)
-    torch.cuda.set_device(device)
-
-    r = measure(wl, B, args.steps, args.warmup, rank, world, dist, args.eager, device)
+    if dry:
+        r = measure_stub(wl, B, args.steps)
+        if dist is not None:
+            dist.barrier()
+        device = None
+    else:
+        # DSP_BENCH_DEVICE pins every rank to one device: a rehearsal of the
+        # multi-rank path on a one-GPU box (the driver's runs leave it unset).
+        dev_index = int(os.environ.get("DSP_BENCH_DEVICE", local_rank))
+        device = torch.device("cuda", dev_index)
+        torch.cuda.set_device(device)
+        r = measure(wl, B, args.steps, args.warmup, rank, world, dist, args.eager, device)
     chain, elapsed, kernels, dom = r["chain"], r["elapsed"], r["kernels"], r["dom"]
+    if dist is not None and dry:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
     value = total * wl["n_in"] * args.steps / elapsed / 1e6
     mean_ms = kernels[dom]
@@ -337,22 +486,22 @@ def main(argv=None):
     chain_bytes = chain.algorithmic_bytes()
     chain_gbs = chain_bytes / (ms_per_step * 1e-3) / 1e9
     launch, n_out, dom_bytes = r["launch"], chain.n_out, r["dom_bytes"]
-    extra3 = None
-    if world == 1 and args.config == "c4" and not args.no_config3:
+    extras = {}
+    if world == 1 and not args.no_extras and not dry:
         del chain, r
         torch.cuda.empty_cache()
-        wl3 = WORKLOADS["c3"]
-        r3 = measure(wl3, wl3["channels"], args.steps, args.warmup, 0, 1, None, args.eager,
-                     device)
-        ms3 = r3["elapsed"] / args.steps * 1e3
-        extra3 = {
-            "workload": wl3["desc"], "channels": wl3["channels"],
-            "value": round(wl3["channels"] * wl3["n_in"] / (ms3 * 1e-3) / 1e6, 2),
-            "unit": "Msamples/s", "ms_per_step": round(ms3, 4),
-            "chain_frac": round(r3["chain"].algorithmic_bytes() / (ms3 * 1e-3) / 1e9
-                                / HBM_PEAK_GBS, 4),
-            "kernels_ms": r3["kernels"],
-        }
+        for key in ("c3", "c4", "c5"):
+            if key == args.config:
+                continue
+            wlx = WORKLOADS[key]
+            rx = measure(wlx, wlx["channels"], args.steps, args.warmup, 0, 1, None, args.eager,
+                         device)
+            extras[wlx["name"]] = extra_line(wlx, rx, args.steps)
+            del rx
+            torch.cuda.empty_cache()
+        extras["host_inclusive"] = host_inclusive(device)
+        extras["copy_ceiling"] = copy_ceiling(device)
+    ceiling = (extras.get("copy_ceiling") or {}).get("value")
 
     if rank == 0:
         out = {
@@ -384,6 +533,8 @@ def main(argv=None):
                 "frac_actual": (round(traffic / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                 if traffic else None),
                 "traffic_source": traffic_src if traffic else None,
+                "copy_ceiling_gbs": ceiling,
+                "frac_vs_copy_ceiling": round(achieved / ceiling, 4) if ceiling else None,
                 "algorithmic_bytes": dom_bytes,
                 "mean_ms": mean_ms,
                 "valu": valu,
@@ -391,10 +542,13 @@ def main(argv=None):
             "chain_roofline": {
                 "achieved": round(chain_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(chain_gbs / HBM_PEAK_GBS, 4),
+                "frac_vs_copy_ceiling": round(chain_gbs / ceiling, 4) if ceiling else None,
                 "algorithmic_bytes_per_gpu_step": chain_bytes,
             },
             "kernels_ms": kernels,
-            "config3": extra3,
+            **{k: extras.get(k) for k in ("config3", "config4", "config5") if k in extras},
+            "host_inclusive": extras.get("host_inclusive"),
+            "copy_ceiling": extras.get("copy_ceiling"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -25,6 +25,10 @@ thread_local TraceState g_trace;
 // dsp_chain_path: 0 single-pass kernel where instantiated (default), 1 always
 // the two-launch chain.
 thread_local int g_chain_path = 0;
+// dsp_chain_spin_limit: polls before a single-pass hand-off wait gives up
+// (2^23 polls with s_sleep 2 between them: ~0.4 s).
+constexpr int64_t kDefaultSpins = (int64_t)1 << 23;
+thread_local int64_t g_spin_limit = kDefaultSpins;
 }  // namespace
 
 TraceScope::TraceScope(const char* name, hipStream_t s) : slot_(-1), s_(s) {
@@ -61,7 +65,13 @@ void clear_error() { g_error.clear(); }
 
 extern "C" {
 
-int dsp_version(void) { return 10300; /* 1.3.0: chain tables with the shifted class rows of k_chain_gct */ }
+int dsp_version(void) {
+  // 2.0.0: dsp_chain_f32 takes the tables' key and y may be NULL;
+  // dsp_chain_tile_tables returns the key; the chain workspace holds the
+  // single-pass region and the cascade's scratch side by side;
+  // dsp_chain_status / dsp_chain_spin_limit added (round 3).
+  return 20000;
+}
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
 
@@ -153,19 +163,41 @@ int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, in
 
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t K, int32_t L,
                                  int32_t M, int64_t c_offset, int32_t S, int64_t chunk_len) {
-  const size_t a = dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
-  const size_t b = dsp::chain_tile_workspace_bytes(B, n_in, n_out, K, L, M, c_offset, S);
-  return a > b ? a : b;
+  // [status header + single-pass hand-off region][two-launch cascade scratch]:
+  // the two paths never share bytes, so switching paths (dsp_chain_path, or a
+  // geometry the single-pass kernel declines) cannot leave stale hand-off flags.
+  const size_t head = dsp::chain_tile_workspace_bytes(B, n_in, n_out, K, L, M, c_offset, S);
+  return head + dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+}
+
+int dsp_chain_status(void* workspace, size_t workspace_bytes, int32_t reset, void* stream) {
+  dsp::clear_error();
+  DSP_REQUIRE(workspace && workspace_bytes >= 4, "null or empty workspace");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t word = 0;
+  DSP_HIP(hipMemcpyAsync(&word, workspace, sizeof(word), hipMemcpyDeviceToHost, s));
+  if (reset) DSP_HIP(hipMemsetAsync(workspace, 0, workspace_bytes, s));
+  DSP_HIP(hipStreamSynchronize(s));
+  return word != 0 ? 1 : 0;
+}
+
+int64_t dsp_chain_spin_limit(int64_t spins) {
+  dsp::clear_error();
+  if (spins < -1 || spins > 0xffffffffll)
+    return dsp::set_error(DSP_EINVAL, "spin limit %lld not in [-1, 2^32)", (long long)spins);
+  const int64_t prev = dsp::g_spin_limit;
+  if (spins >= 0) dsp::g_spin_limit = spins;
+  return prev;
 }
 
 size_t dsp_chain_tile_tables_bytes(void) { return dsp::chain_tile_tables_bytes(); }
 
 int dsp_chain_tile_tables(void* tables_host, size_t tables_bytes, int64_t n_in, int64_t n_out,
                           const float* taps_host, int32_t K, int32_t L, int32_t M,
-                          int64_t c_offset, const double* sos_host, int32_t S) {
+                          int64_t c_offset, const double* sos_host, int32_t S, uint64_t* key) {
   dsp::clear_error();
   return dsp::chain_tile_tables(tables_host, tables_bytes, n_in, n_out, taps_host, K, L, M,
-                                c_offset, sos_host, S);
+                                c_offset, sos_host, S, key);
 }
 
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
@@ -180,25 +212,35 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                   int32_t L, int32_t M, int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
                   const double* xstate_table, int64_t xstate_rows, const void* tile_tables,
-                  int64_t seg_start,
+                  uint64_t tile_key, int64_t seg_start,
                   int64_t seg_len, int32_t log2n, int64_t ld_mag, const float* window,
                   const float* twiddles, void* workspace, size_t workspace_bytes,
                   void* stream) {
   dsp::clear_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
+  if (y && y == z) return dsp::set_error(DSP_EINVAL, "y and z must not alias");
   if (log2n < 0 || log2n > DSP_MAX_LOG2N)
     return dsp::set_error(DSP_EINVAL, "chain spectrum log2n=%d outside [0, %d]", log2n,
                           DSP_MAX_LOG2N);
   if (B == 0) return DSP_OK;
+  const size_t head = dsp::chain_tile_workspace_bytes(B, n_in, n_out, K, L, M, c_offset, S);
+  DSP_REQUIRE(workspace && workspace_bytes >= head,
+              "chain workspace too small: %zu < %zu bytes (dsp_chain_workspace_bytes)",
+              workspace_bytes, head);
   int rc = dsp::kNotFused;
   if (dsp::g_chain_path == 0)
     rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
-                                sos_host, S, clip, tile_tables, workspace, workspace_bytes, s);
+                                sos_host, S, clip, tile_tables, tile_key,
+                                (uint32_t)dsp::g_spin_limit, workspace, head, s);
   if (rc == dsp::kNotFused) {
     // Two-launch chain: SRC, then the cascade with x-domain chunk states where
     // the input rows are aligned and the chunking fits, else the y-domain
-    // table (include/dspcore.h).
+    // table (include/dspcore.h).  y carries the SRC output between the two.
+    if (!y)
+      return dsp::set_error(DSP_EINVAL, "y == NULL needs the single-pass kernel (dsp_chain_tile_len "
+                                        "> 0, its tables and key, dsp_chain_path 0)");
+    char* scratch = static_cast<char*>(workspace) + head;
+    const size_t scratch_bytes = workspace_bytes - head;
     rc = dsp::launch_src(x, y, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset, s);
     if (rc) return rc;
     if (xstate_table && dsp::xstate_applicable(n_out, S, chunk_len, x, ld_x, L, M))
@@ -206,7 +248,7 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                                      n_in, ld_x, K, L, M, c_offset, xstate_table, xstate_rows, s);
     else
       rc = dsp::launch_biquad(y, z, B, n_out, ld_y, ld_y, sos_host, S, clip, chunk_len,
-                              state_table, workspace, workspace_bytes, s);
+                              state_table, scratch_bytes ? scratch : nullptr, scratch_bytes, s);
   }
   if (rc) return rc;
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,

@@ -19,9 +19,13 @@
 //      window, read from the tile's x window in LDS (one coalesced load per
 //      tile, padded so the 64 lanes' ds_read_b128 are conflict-free).  Same
 //      per-output FMA order as k_src_reg: y is bitwise the SRC kernel's.
-//   2. pass 1: the sub-chunk's zero-state end state, in block-diagonal
-//      coordinates (below): E'_l = sum_i G'[i] y[i], G'[i] = T^-1 A^(TSUB-1-i) B
-//      (wave-uniform, float64), 12 FMAs per sample;
+//   2. pass 1: the sub-chunk's zero-state end state.  The sums run in float32
+//      (v_pk_fma_f32, 6 per sample) in INPUT-NORMAL coordinates xi = P^-1 w
+//      (P P^T = the cascade's state covariance under unit white noise, so every
+//      coordinate has unit variance and the float32 sums do not cancel):
+//      e_l = sum_i Gc[i] y[i], Gc[i] = P^-1 A^(TSUB-1-i) B (wave-uniform);
+//      then one float64 change of basis E'_l = Q e_l, Q = T^-1 P (lower
+//      triangular, 78 FMAs per lane), into block-diagonal coordinates (below);
 //   3. carry: the tile's entry state m_in comes from the previous tile of the
 //      same channel (chained hand-off, below); an inclusive Kogge-Stone scan
 //      across the 64 lanes, v_l += D^(TSUB 2^d) v_(l-2^d) for d = 0..5, gives
@@ -50,13 +54,17 @@
 // chip's resident wave count its end state is normally published long before
 // tile t needs it.  A workgroup waits only on a lower id, and ids are
 // dispatched in order, so every wait ends.  The state (12 doubles) and its
-// flag follow the agent-scope hand-off the gfx950 guide measures valid: the
-// producer's lanes store the payload with sc1 stores, wait vmcnt(0), then one
-// lane stores the flag sc1; the consumer polls the flag with sc1 loads and then
-// loads the payload with sc1 loads.  The consumer clears the flag, so a
-// completed launch leaves the flag array zero for the next one (the caller
-// zero-fills the workspace once).  A wait that exceeds ~1 s (a broken dispatch
-// order) gives up, marks the workspace's error word and continues: no hang.
+// flag are an agent-scope release/acquire pair: the producer lane stores the
+// payload (sc1), fences (release, agent: buffer_wbl2 sc1 + vmcnt(0)) and stores
+// the flag; the consumer polls the flag (relaxed, sc1), fences (acquire,
+// agent: buffer_inv sc1) and loads the payload.  The consumer clears the flag,
+// so a completed launch leaves the flag array zero for the next one (the
+// caller zero-fills the workspace once).  A wait that polls more than the
+// thread's spin limit (dsp_chain_spin_limit; default 2^23 polls with
+// s_sleep 2 between them, ~0.4 s: a broken dispatch order, or a GPU
+// time-sliced between processes) gives up: it sets the workspace's status word
+// (dsp_chain_status reports it, Chain.run raises) and leaves the flag for the
+// workspace reset; z of that launch is wrong, nothing hangs.
 //
 // Rows are bitwise independent of the batch size: the geometry depends on
 // (L, M, K) only.
@@ -76,7 +84,7 @@ constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
-constexpr uint32_t kMaxSpins = 1u << 23;  // x s_sleep 2 (128 clk): ~0.4 s
+
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -141,11 +149,14 @@ constexpr int kCtClassStride = kGenTS * kCtRow + 4;  // 388: class rows on disti
 // Tables of the single-pass kernel, built on the host in float64
 // (dsp_chain_tile_tables) and read by the kernel through the scalar cache.
 struct TileTables {
+  uint64_t key;            // dsp_chain_tile_tables' fingerprint of what they were built for
   double G[64][kD];        // G'[i] = T^-1 A^(TSUB-1-i) B, i < TSUB (block-diagonal coords)
+  float Gc[32][kD][2];     // Gc[j][d] = rows 2j, 2j+1 of P^-1 A^(TSUB-1-i) B (input-normal), float32
+  double Q[kD][kD];        // T^-1 P, lower triangular (input-normal -> block-diagonal)
   double Dp[6][kS][4];     // D_k^(TSUB 2^d), row-major 2x2, d = 0..5
   double T[kD][kD];        // s = T m (row-major; zero rows/cols: padding stages)
   float TP[kNPMax][4][2];  // tap pairs: TP[p][ph] = (h[2p - a_ph], h[2p + 1 - a_ph])
-  int32_t tsub, np, L, M, K, S;  // what the tables were built for (checked at launch)
+  int32_t tsub, np, L, M, K, S;  // what the tables were built for (in `key`)
   // The DF2 realisation (cascade.h, NORM form): per stage {c1, c2, a1, a2}
   // and the input gain.  Read through the scalar cache right where pass 2
   // needs them instead of occupying ~50 SGPRs as kernel arguments for the
@@ -175,9 +186,10 @@ struct TileArgs {
   const TileTables* tt;     // device copy of dsp_chain_tile_tables' output
   double* states;           // [B][ntiles][12] tile end states (block-diagonal coords)
   uint32_t* flags;          // [B][ntiles]
-  uint32_t* err;            // set when a hand-off wait gave up
+  uint32_t* err;            // workspace status word: set when a hand-off wait gave up
   int64_t B, n_in, ld_x, n_out, ld_y, ntiles, cq;
   int clip;
+  uint32_t max_spins;       // polls before a hand-off wait gives up
   // generic kernel (k_chain_gen) only
   const float* taps;        // device taps [K]
   int64_t c;                // 'same' offset of the expanded convolution
@@ -319,8 +331,10 @@ template <int TS>
 __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
                                              float (&y)[TS], int lane, int64_t b, int64_t tile,
                                              int64_t m0) {
-  // ---- 2. pass 1: zero-state end state of the sub-chunk, block-diagonal coords
+  // ---- 2. pass 1: zero-state end state of the sub-chunk
   double v[kD];
+#if DSP_P1_F64
+  // float64 sums in block-diagonal coordinates (round 2; A/B reference)
 #pragma unroll
   for (int d = 0; d < kD; ++d) v[d] = 0.0;
 #pragma unroll
@@ -329,6 +343,50 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #pragma unroll
     for (int d = 0; d < kD; ++d) v[d] = fma(mt->G[i][d], u, v[d]);
   }
+#else
+  {
+    // float32 sums in input-normal coordinates: component d keeps the sums
+    // over even and odd samples in the halves of one v_pk_fma_f32 chain
+    // (samples 2j, 2j+1 against the row pair Gc[j][d]) ...
+    f32x2 e2[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) e2[d] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < TS / 2; ++j) {
+      // Each row pair's 24 floats are scalar-loaded right before its FMAs (an
+      // opaque table pointer per pair keeps the compiler from hoisting the
+      // whole table into SGPRs, which spills).
+      tt_ptr tq = mt;
+      asm volatile("" : "+s"(tq));
+      const f32x2 u = f32x2{y[2 * j], y[2 * j + 1]};
+#pragma unroll
+      for (int d = 0; d < kD; ++d)
+        e2[d] = __builtin_elementwise_fma(f32x2{tq->Gc[j][d][0], tq->Gc[j][d][1]}, u, e2[d]);
+    }
+    pin(e2);
+    f32x2 e[kS];
+#pragma unroll
+    for (int k = 0; k < kS; ++k)
+      e[k] = f32x2{e2[2 * k].x + e2[2 * k].y, e2[2 * k + 1].x + e2[2 * k + 1].y};
+    // ... then E' = Q e in float64 (Q lower triangular; rows from the last,
+    // so that e_r dies after row r: 12 doubles live, not 24).
+    double ed[kD];
+#pragma unroll
+    for (int k = 0; k < kS; ++k) {
+      ed[2 * k] = (double)e[k].x;
+      ed[2 * k + 1] = (double)e[k].y;
+    }
+#pragma unroll
+    for (int r = kD - 1; r >= 0; --r) {
+      tt_ptr tq = mt;
+      asm volatile("" : "+s"(tq));
+      double acc = tq->Q[r][0] * ed[0];
+#pragma unroll
+      for (int c = 1; c <= r; ++c) acc = fma(tq->Q[r][c], ed[c], acc);
+      v[r] = acc;
+    }
+  }
+#endif
   // Keep the SRC and pass 1 ahead of the hand-off wait (the compiler would
   // otherwise sink them past it).
   pin(v);
@@ -340,17 +398,24 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   if (tile > 0 && lane == 0) {
     const int64_t prev = b * a.ntiles + tile - 1;
     uint32_t spins = 0;
+    bool ok = true;
     while (load_flag(a.flags + prev) == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins == kMaxSpins) {
+      if (++spins > a.max_spins) {
+        // Give up: mark the status word; the flag stays for the workspace
+        // reset (a late producer would set it again anyway).
         store_flag(a.err, 1u);
+        ok = false;
         break;
       }
+      __builtin_amdgcn_s_sleep(2);
     }
+#if !DSP_HANDOFF_RELAXED
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     fence();
 #pragma unroll
     for (int d = 0; d < kD; ++d) m_in[d] = load_state(a.states + prev * kD + d);
-    store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
+    if (ok) store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
     // v_0 = D^TSUB m_in + E'_0
 #pragma unroll
     for (int k = 0; k < kS; ++k)
@@ -391,14 +456,21 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     const int64_t me = b * a.ntiles + tile;
 #pragma unroll
     for (int d = 0; d < kD; ++d) store_state(a.states + me * kD + d, v[d]);
+#if DSP_HANDOFF_RELAXED
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     store_flag(a.flags + me, 1u);
   }
 
-  // ---- 5. y out, DF2 entry state s = T m, pass 2, z out
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-  store_tile<TS>(lds, y, lane, ry, m0);
+  // ---- 5. y out (unless the caller passed y = NULL), DF2 entry state
+  // s = T m, pass 2, z out
+  if (a.y) {
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+    store_tile<TS>(lds, y, lane, ry, m0);
+  }
   pin(y);
   // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
   // rows and columns for padding stages), so row r starts from m[r].
@@ -816,6 +888,26 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Fingerprint of everything the tables depend on that a call can state on the
+// host: the kernel kind and geometry, the cascade (sos bits) and the table
+// layout version.  FNV-1a, 64 bit.
+uint64_t tables_key(const TilePlan& tp, int64_t n_in, int64_t n_out, int K, int L, int M,
+                    int64_t c, const double* sos, int S) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) {
+      h ^= b[i];
+      h *= 1099511628211ull;
+    }
+  };
+  const int64_t v[] = {2 /* table layout version */, tp.kind, tp.tsub, n_in, n_out, K, L, M, c, S,
+                       (int64_t)sizeof(TileTables)};
+  mix(v, sizeof(v));
+  if (S > 0 && sos) mix(sos, sizeof(double) * 5 * (size_t)S);
+  return h ? h : 1;  // 0 never names a table
+}
+
 // Solves the 4x4 system M z = r in place (partial pivoting); false if singular
 // to working precision.
 bool solve4(double M[4][4], double r[4]) {
@@ -839,6 +931,104 @@ bool solve4(double M[4][4], double r[4]) {
     for (int j = c + 1; j < 4; ++j) s -= M[c][j] * r[j];
     r[c] = s / M[c][c];
   }
+  return true;
+}
+
+// Pass-1 tables in input-normal coordinates (file comment, step 2): the state
+// covariance of the first n states under unit white noise, X = sum_k A^k B B^T
+// A^kT (doubling: X <- X + P X P^T, P <- P^2), its Cholesky factor P (X = P
+// P^T), Gc[i] = P^-1 A^(tsub-1-i) B in float32 and Q = T^-1 P.  Any
+// invertible P gives the exact E' in float64 arithmetic; input-normal
+// coordinates keep the float32 sums well scaled.  false when X is not
+// numerically positive definite (an uncontrollable mode, e.g. a band cancelled
+// by its inverse) or P is ill-conditioned: the two-launch chain serves those.
+bool input_normal_tables(const std::vector<double>& A, const double* Bv,
+                         const std::vector<double>& Ti, int n, int tsub, TileTables* tt) {
+  if (n == 0) return true;  // no real stage: pass 1 sums nothing
+  auto at = [&](const std::vector<double>& M, int r, int c) -> double { return M[(size_t)r * kD + c]; };
+  std::vector<double> X((size_t)kD * kD, 0.0), Pw(A), tmp((size_t)kD * kD);
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) X[(size_t)r * kD + c] = Bv[r] * Bv[c];
+  for (int it = 0; it < 40; ++it) {
+    // X += Pw X Pw^T
+    double pmax = 0.0;
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < n; ++k) acc += at(Pw, r, k) * at(X, k, c);
+        tmp[(size_t)r * kD + c] = acc;
+      }
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < n; ++k) acc += at(tmp, r, k) * at(Pw, c, k);
+        X[(size_t)r * kD + c] += acc;
+      }
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < n; ++k) acc += at(Pw, r, k) * at(Pw, k, c);
+        tmp[(size_t)r * kD + c] = acc;
+        pmax = std::max(pmax, std::fabs(acc));
+      }
+    Pw.swap(tmp);
+    if (pmax < 1e-30) break;
+  }
+  // Cholesky X = P P^T (lower).
+  std::vector<double> P((size_t)kD * kD, 0.0), Pi((size_t)kD * kD, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = at(X, j, j);
+    for (int k = 0; k < j; ++k) d -= at(P, j, k) * at(P, j, k);
+    if (!(d > 1e-24 * at(X, j, j)) || !(d > 0.0)) return false;
+    const double pj = std::sqrt(d);
+    P[(size_t)j * kD + j] = pj;
+    for (int i = j + 1; i < n; ++i) {
+      double v = at(X, i, j);
+      for (int k = 0; k < j; ++k) v -= at(P, i, k) * at(P, j, k);
+      P[(size_t)i * kD + j] = v / pj;
+    }
+  }
+  // P^-1 (lower triangular, forward substitution per column).
+  for (int c = 0; c < n; ++c)
+    for (int r = c; r < n; ++r) {
+      double v = (r == c) ? 1.0 : 0.0;
+      for (int k = c; k < r; ++k) v -= at(P, r, k) * at(Pi, k, c);
+      Pi[(size_t)r * kD + c] = v / at(P, r, r);
+    }
+  double nP = 0.0, nPi = 0.0;
+  for (int r = 0; r < n; ++r) {
+    double a = 0.0, b = 0.0;
+    for (int c = 0; c < n; ++c) {
+      a += std::fabs(at(P, r, c));
+      b += std::fabs(at(Pi, r, c));
+    }
+    nP = std::max(nP, a);
+    nPi = std::max(nPi, b);
+  }
+  if (!(nP * nPi < 1e8)) return false;
+  // Gc[i] = P^-1 A^(tsub-1-i) B, i = tsub-1 down to 0.
+  std::vector<double> g(Bv, Bv + kD), gn(kD);
+  for (int i = tsub - 1; i >= 0; --i) {
+    for (int r = 0; r < kD; ++r) {
+      double v = 0.0;
+      for (int c = 0; c < n && r < n; ++c) v += at(Pi, r, c) * g[c];
+      tt->Gc[i / 2][r][i % 2] = (float)v;
+    }
+    for (int r = 0; r < n; ++r) {
+      double v = 0.0;
+      for (int c = 0; c < n; ++c) v += at(A, r, c) * g[c];
+      gn[r] = v;
+    }
+    for (int r = 0; r < n; ++r) g[r] = gn[r];
+  }
+  // Q = T^-1 P (both lower triangular).
+  for (int r = 0; r < kD; ++r)
+    for (int c = 0; c < kD; ++c) {
+      double v = 0.0;
+      if (r < n && c < n)
+        for (int k = c; k <= r; ++k) v += at(Ti, r, k) * at(P, k, c);
+      tt->Q[r][c] = v;
+    }
   return true;
 }
 
@@ -942,7 +1132,7 @@ bool modal_tables(const SosParams& p, int Sr, int tsub, TileTables* tt) {
   }
   for (int r = 0; r < kD; ++r)
     for (int c = 0; c < kD; ++c) tt->T[r][c] = (r < n && c < n) ? T[(size_t)r * kD + c] : 0.0;
-  return true;
+  return input_normal_tables(A, Bv, Ti, n, tsub, tt);
 }
 
 // Tap pairs of the packed SRC: branch ph, pair p = (h[2p - a], h[2p + 1 - a])
@@ -1026,15 +1216,17 @@ int64_t chain_tile_sub(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t
 
 size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M,
                                   int64_t c, int S) {
+  // The status header (256 B, word 0: hand-off status) always exists.
   TilePlan tp;
-  if (B <= 0 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 0;
+  if (B <= 0 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 256;
   return tile_ws(B, tp.ntiles).total;
 }
 
 size_t chain_tile_tables_bytes() { return sizeof(TileTables); }
 
 int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, const float* taps,
-                      int K, int L, int M, int64_t c, const double* sos, int S) {
+                      int K, int L, int M, int64_t c, const double* sos, int S, uint64_t* key) {
+  if (key) *key = 0;
   TilePlan tp;
   if (!tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
   DSP_REQUIRE(out && out_bytes >= sizeof(TileTables), "tables buffer too small: %zu < %zu bytes",
@@ -1063,19 +1255,23 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   tt->M = M;
   tt->K = K;
   tt->S = S;
+  tt->key = tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
+  if (key) *key = tt->key;
   return DSP_OK;
 }
 
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
                       int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
-                      int64_t c, const double* sos, int S, int clip, const void* tables, void* ws,
-                      size_t ws_bytes, hipStream_t s) {
+                      int64_t c, const double* sos, int S, int clip, const void* tables,
+                      uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s) {
   TilePlan tp;
   if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
+  // Tables built for another geometry or cascade: the two-launch chain.
+  if (key != tables_key(tp, n_in, n_out, K, L, M, c, sos, S)) return kNotFused;
   auto aligned = [](const void* p, int64_t ld) {
     return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   };
-  if (!aligned(x, ld_x) || !aligned(y, ld_y) || !aligned(z, ld_y)) return kNotFused;
+  if (!aligned(x, ld_x) || (y && !aligned(y, ld_y)) || !aligned(z, ld_y)) return kNotFused;
   SosParams p;
   if (S > 0 && !realize(sos, S, &p)) return kNotFused;
   if (S == 0) realize(nullptr, 0, &p);
@@ -1102,6 +1298,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.ntiles = tp.ntiles;
   a.cq = c / L;
   a.clip = clip;
+  a.max_spins = max_spins;
   a.taps = taps;
   a.c = c;
   a.K = K;

@@ -120,11 +120,14 @@ size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K,
                                   int64_t c, int S);
 size_t chain_tile_tables_bytes();
 int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, const float* taps,
-                      int K, int L, int M, int64_t c, const double* sos, int S);
+                      int K, int L, int M, int64_t c, const double* sos, int S, uint64_t* key);
+// y may be NULL (the y store is skipped).  Returns kNotFused (nothing
+// launched) when the kernel does not serve the call or `key` is not the
+// fingerprint of tables built for it.
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
                       int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
-                      int64_t c, const double* sos, int S, int clip, const void* tables, void* ws,
-                      size_t ws_bytes, hipStream_t s);
+                      int64_t c, const double* sos, int S, int clip, const void* tables,
+                      uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s);
 // Whether launch_biquad_xstate's conditions on the cascade (n, S, chunk_len)
 // and on the SRC input rows (16-byte aligned) hold.
 bool xstate_applicable(int64_t n, int S, int64_t chunk_len, const float* xs, int64_t ld_xs,

@@ -32,7 +32,7 @@ DSP_MAX_LOG2N = 14
 DSP_MAX_LOG2N_FFT = 22
 DSP_MAX_DFT = 8192
 
-_c_i32, _c_i64, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+_c_i32, _c_i64, _c_u64, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
 _vp, _dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
 
 # name -> (restype, argtypes); mirrors include/dspcore.h one to one.
@@ -61,10 +61,13 @@ _SIGNATURES = {
     "dsp_chain_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
         _c_i32, _c_i32, _c_i32, _c_i64, _dp, _c_i32, _c_i32, _c_i64, _vp, _vp, _c_i64,
-        _vp, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+        _vp, _c_u64, _c_i64, _c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "dsp_chain_tile_tables_bytes": (_c_sz, []),
     "dsp_chain_tile_tables": (ctypes.c_int, [_vp, _c_sz, _c_i64, _c_i64, _vp, _c_i32, _c_i32,
-                                             _c_i32, _c_i64, _dp, _c_i32]),
+                                             _c_i32, _c_i64, _dp, _c_i32,
+                                             ctypes.POINTER(_c_u64)]),
+    "dsp_chain_status": (ctypes.c_int, [_vp, _c_sz, _c_i32, _vp]),
+    "dsp_chain_spin_limit": (_c_i64, [_c_i64]),
     "dsp_chain_path": (ctypes.c_int, [_c_i32]),
     "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,
@@ -148,6 +151,15 @@ def chain_path(path: int = -1) -> int:
     if rc < 0:
         check(rc, "dsp_chain_path")
     return rc
+
+
+def spin_limit(spins: int = -1) -> int:
+    """Polls before a single-pass hand-off wait gives up, on the calling
+    thread (dsp_chain_spin_limit); -1 only queries.  Returns the previous one."""
+    rc = load().dsp_chain_spin_limit(int(spins))
+    if rc < 0:
+        check(int(rc), "dsp_chain_spin_limit")
+    return int(rc)
 
 
 def trace_enable(on: bool) -> None:

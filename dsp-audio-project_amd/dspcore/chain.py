@@ -7,9 +7,15 @@ A Chain owns every device buffer (taps, LUTs, y, z, mag, workspace) so that
 Where the library has a single-pass kernel for the geometry
 (dsp_chain_tile_len > 0, include/dspcore.h) one launch computes y and z from x
 and a second the spectrum; otherwise SRC, cascade and spectrum run as three.
+
+The single-pass kernel hands each tile's carry to the next tile through the
+workspace; if a wait ever gives up (dsp_chain_status), run() raises
+HandoffError after re-zeroing the workspace, so corrupted z never reaches a
+caller that checks (the default outside graph capture).
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -18,6 +24,11 @@ import torch
 from . import _lib, ops
 from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, max_chunks_for,
                      spectrum_plan, src_plan, xstate_chunk_len)
+
+
+class HandoffError(RuntimeError):
+    """A single-pass tile hand-off wait gave up: that call's z is wrong
+    (include/dspcore.h, dsp_chain_status).  The workspace has been reset."""
 
 
 @dataclass(frozen=True)
@@ -37,11 +48,15 @@ class Chain:
 
     def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
                  chunk_len: int | None = None, use_table: bool = True,
-                 use_xstate: bool = True, plan_batch: int | None = None):
+                 use_xstate: bool = True, plan_batch: int | None = None,
+                 keep_y: bool = True):
         """plan_batch: the batch size the cascade's chunking is planned for
         (default: `batch`).  Shards of one job pass the job's total batch so
         that every shard runs the same chunking and the rows come out bitwise
-        equal to the unsharded run (design.max_chunks_for)."""
+        equal to the unsharded run (design.max_chunks_for).
+        keep_y=False: run() returns (None, z, mag) and, where the single-pass
+        kernel serves the geometry, y is never written (dsp_chain_f32 with
+        y = NULL); otherwise y lives in an internal buffer."""
         ops.require_gpu()
         self.cfg = cfg
         self.B = int(batch)
@@ -84,9 +99,9 @@ class Chain:
         # single-pass kernel's float4 stores apply to every n_out; y and z are
         # [B, n_out] views of the padded buffers.
         ld = -(-n_out // 4) * 4
-        self._ybuf = torch.empty((self.B, ld), dtype=torch.float32, device=dev)
+        self._ld = ld
+        self.keep_y = bool(keep_y)
         self._zbuf = torch.empty((self.B, ld), dtype=torch.float32, device=dev)
-        self.y = self._ybuf[:, :n_out]
         self.z = self._zbuf[:, :n_out]
         self.mag = torch.empty((self.B, self.spec.n_fft // 2 + 1), dtype=torch.float32,
                                device=dev)
@@ -99,20 +114,31 @@ class Chain:
         # Single-pass kernel tables (dsp_chain_tile_tables): built once on the
         # host in float64 from the float32 taps and the sos, kept on the device.
         self.tile_tables = None
+        self.tile_key = 0
         if self.tile_len > 0:
             nbytes = int(lib.dsp_chain_tile_tables_bytes())
             host = np.zeros(nbytes, dtype=np.uint8)
             taps32 = np.ascontiguousarray(self.src.taps, dtype=np.float32)
+            key = ctypes.c_uint64(0)
             rc = lib.dsp_chain_tile_tables(
                 host.ctypes.data, nbytes, cfg.n_in, n_out, taps32.ctypes.data, self.src.K,
-                self.src.L, self.src.M, self.src.c_offset, _lib.sos_pointer(self.sos), S)
+                self.src.L, self.src.M, self.src.c_offset, _lib.sos_pointer(self.sos), S,
+                ctypes.byref(key))
             if rc < 0:
                 _lib.check(rc, "dsp_chain_tile_tables")
             if rc == 0:
                 # 256-byte aligned device copy (torch's allocator aligns to 512 B)
                 self.tile_tables = torch.from_numpy(host).to(dev)
+                self.tile_key = int(key.value)
             else:
                 self.tile_len = 0
+        # y: the caller's output, or the two-launch chain's intermediate; with
+        # keep_y=False on the single-pass path it is never allocated.
+        if self.keep_y or self.tile_len == 0:
+            self._ybuf = torch.empty((self.B, self._ld), dtype=torch.float32, device=dev)
+            self.y = self._ybuf[:, :n_out]
+        else:
+            self._ybuf = self.y = None
         self.xtable, self.xrows = (ops.xstate_table(self.sos, self.src, self.chunk_len, dev)
                                    if self.xstate else (None, 0))
 
@@ -122,10 +148,29 @@ class Chain:
         per = 4 * self.cfg.n_in + 8 * self.n_out + 4 * (self.spec.n_fft // 2 + 1)
         return per * self.B
 
+    def _status(self, reset: bool) -> int:
+        lib = _lib.load()
+        with torch.cuda.device(self.device):
+            rc = lib.dsp_chain_status(self.workspace.data_ptr(), self.workspace.numel(),
+                                      int(bool(reset)),
+                                      torch.cuda.current_stream(self.device).cuda_stream)
+        if rc < 0:
+            _lib.check(rc, "dsp_chain_status")
+        return rc
+
     def handoff_ok(self) -> bool:
-        """False if a single-pass call's tile hand-off wait gave up (workspace
-        word 0, include/dspcore.h); synchronises the device."""
-        return int(self.workspace[:4].view(torch.int32).item()) == 0
+        """False if a single-pass call's tile hand-off wait gave up since the
+        last reset (dsp_chain_status; synchronises the stream)."""
+        return self._status(False) == 0
+
+    def check(self) -> None:
+        """Raises HandoffError (after re-zeroing the workspace, so the next
+        call starts clean) if a tile hand-off wait gave up since the last
+        check; synchronises the stream."""
+        if self._status(False):
+            self._status(True)
+            raise HandoffError("single-pass chain: a tile hand-off wait gave up; z of the "
+                               "last call(s) is wrong (workspace reset; rerun the call)")
 
     def check_input(self, x: torch.Tensor) -> torch.Tensor:
         if x.shape != (self.B, self.cfg.n_in) or x.dtype != torch.float32 or not x.is_cuda:
@@ -135,29 +180,41 @@ class Chain:
             x = x.contiguous()
         return x
 
-    def run(self, x: torch.Tensor):
-        """One fused-call pass: y = SRC(x), z = EQ(y), mag = |FFT(hann*z[seg])|."""
+    def run(self, x: torch.Tensor, check: bool | None = None):
+        """One fused-call pass: y = SRC(x), z = EQ(y), mag = |FFT(hann*z[seg])|.
+
+        check: read the hand-off status after the launches and raise
+        HandoffError if a wait gave up (synchronises the stream).  None (the
+        default) checks unless the stream is being captured into a graph;
+        callers that replay graphs or pipeline many calls pass False and call
+        check() themselves."""
         x = self.check_input(x)
         if self.identity_src:
             # SRC bypass (dsp_core.py:144-145): y is x itself.
             self.run_stages(x)
-            return x, self.z, self.mag
+            return (x if self.keep_y else None), self.z, self.mag
         lib = _lib.load()
         sos_ptr = _lib.sos_pointer(self.sos)
         S = self.sos.shape[0]
         clip = 0 if self.eq.bypass else 1
+        y_ptr = self.y.data_ptr() if self.y is not None else None
         with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device)
             rc = lib.dsp_chain_f32(
-                x.data_ptr(), self.y.data_ptr(), self.z.data_ptr(), self.mag.data_ptr(),
-                self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.y),
+                x.data_ptr(), y_ptr, self.z.data_ptr(), self.mag.data_ptr(),
+                self.B, self.cfg.n_in, ops.ld(x), self.n_out, ops.ld(self.z),
                 self.taps.data_ptr(), self.src.K, self.src.L, self.src.M, self.src.c_offset,
                 sos_ptr, S, clip, self.chunk_len, ops._ptr(self.table), ops._ptr(self.xtable),
-                self.xrows, ops._ptr(self.tile_tables), self.spec.seg_start, self.spec.seg_len,
-                self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
+                self.xrows, ops._ptr(self.tile_tables), self.tile_key, self.spec.seg_start,
+                self.spec.seg_len, self.spec.n_fft.bit_length() - 1, ops.ld(self.mag),
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
-                self.workspace.numel(), torch.cuda.current_stream(self.device).cuda_stream)
-        _lib.check(rc, "dsp_chain_f32")
-        return self.y, self.z, self.mag
+                self.workspace.numel(), stream.cuda_stream)
+            _lib.check(rc, "dsp_chain_f32")
+            if check is None:
+                check = self.tile_len > 0 and not torch.cuda.is_current_stream_capturing()
+            if check:
+                self.check()
+        return (self.y if self.keep_y else None), self.z, self.mag
 
     def run_stages(self, x: torch.Tensor, events: list | None = None):
         """Same pass, one entry point per stage; optional (start, end) event pairs

@@ -158,9 +158,12 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *                                     clip == 0 is the EQ bypass: z := y)
  *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
  * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes();
- * the workspace must be zero-filled before its first use, and every completed
- * call leaves it ready for the next one.  Each row's result is bitwise
- * independent of B.
+ * the workspace must be zero-filled before its first use, and every call that
+ * completes with status 0 (dsp_chain_status) leaves it ready for the next one,
+ * whichever path served it: its first 256 bytes are a status header (word 0),
+ * followed by the single-pass kernel's hand-off region, followed by the
+ * two-launch cascade's scratch; the two paths never share bytes.  Each row's
+ * result is bitwise independent of B.
  *
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
  * S <= 6 with every b0 != 0, n_in a multiple of 4, not the SRC bypass, and
@@ -173,25 +176,44 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *       K = 1023: 5 classes; 160/147 itself runs a compile-time-ratio
  *       instantiation whose class rows carry the window shift),
  * `tile_tables` is a device copy (256-byte aligned) of the tables
- * dsp_chain_tile_tables built for this call's geometry, taps and sos, and the
- * rows of x, y and z are 16-byte aligned with pitches that are multiples of 4
- * (n_out itself need not be), ONE kernel computes y and z from x: x is read
- * once, y and z are written once, y is never read back.  Its y is bitwise
- * that of dsp_src_polyphase_f32; z equals the two-launch chain's to float64
- * rounding.
- * chunk_len, state_table and xstate_table are not used by it.  Workspace word
- * 0 (uint32) is nonzero after a call whose tile hand-off wait gave up (a broken
- * dispatch order; z is then wrong): a diagnostic, normally 0.
+ * dsp_chain_tile_tables built for this call's geometry, taps and sos,
+ * `tile_key` is the key it returned with them (a call whose n_in, n_out, K,
+ * L, M, c_offset, S or sos differ from the tables' has another key and takes
+ * the two-launch path; the taps must be the ones the tables were built from),
+ * and the rows of x, y and z are 16-byte aligned with pitches that are
+ * multiples of 4 (n_out itself need not be), ONE kernel computes y and z from
+ * x: x is read once, y and z are written once, y is never read back.  Its y
+ * is bitwise that of dsp_src_polyphase_f32; z agrees with the two-launch
+ * chain's within 2e-6 (its carry sums run in float32 in input-normal
+ * coordinates).  y may be NULL on this path only: the y store
+ * is skipped (a caller that needs z and |Z| alone); anywhere else y == NULL is
+ * DSP_EINVAL.  chunk_len, state_table and xstate_table are not used by it; the
+ * sos host array only keys the tables (the kernel reads its coefficients from
+ * them).
+ *
+ * The single-pass kernel hands each tile's end state to the next tile of the
+ * channel through the workspace; a wait that polls more than the calling
+ * thread's spin limit gives up, sets workspace word 0 and leaves that call's z
+ * wrong (nothing hangs).  dsp_chain_status(workspace, bytes, reset, stream)
+ * synchronises `stream`, returns 0 when word 0 is clear and 1 when a wait gave
+ * up since the last reset (negative DSP_E* on error) and, with reset != 0,
+ * zero-fills the whole workspace (required after a give-up: flags of the
+ * failed call may be left set).  Not graph-capturable.
+ * dsp_chain_spin_limit(spins) sets the calling thread's limit (0 gives up at
+ * the first unanswered poll: a test hook; -1 queries) and returns the previous
+ * one (default 2^23 polls, ~0.4 s).
  *
  * dsp_chain_tile_tables (HOST, no device work) fills `tables_host`
  * (>= dsp_chain_tile_tables_bytes()) with the single-pass kernel's float64
  * carry tables (the cascade in block-diagonal coordinates: the sub-chunk
  * state-response rows, the powers of the diagonal blocks, the change of basis)
  * and, for the 48-sample kernel, its packed tap pairs (for the 32-sample
- * kernel, its per-class tap rows), from the HOST float32 taps and sos.  Returns 0 when the single-pass kernel serves the geometry
- * (copy the buffer to the device once and pass it to every call), 1 when it
- * does not (the two-launch path serves it; nothing to copy), DSP_EINVAL on bad
- * arguments.  With tile_tables == NULL dsp_chain_f32 takes the two-launch path.
+ * kernel, its per-class tap rows), from the HOST float32 taps and sos, and
+ * stores their key in *key (may be NULL).  Returns 0 when the single-pass
+ * kernel serves the geometry (copy the buffer to the device once and pass it
+ * and the key to every call), 1 when it does not (the two-launch path serves
+ * it; nothing to copy; *key = 0), DSP_EINVAL on bad arguments.  With
+ * tile_tables == NULL dsp_chain_f32 takes the two-launch path.
  *
  * Two-launch path (any other geometry, or dsp_chain_path(1)): SRC, then the
  * cascade.  With `xstate_table` (device, float64 [xstate_rows][2S], may be
@@ -220,7 +242,9 @@ size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t
 size_t dsp_chain_tile_tables_bytes(void);
 int dsp_chain_tile_tables(void* tables_host, size_t tables_bytes, int64_t n_in, int64_t n_out,
                           const float* taps_host, int32_t K, int32_t L, int32_t M,
-                          int64_t c_offset, const double* sos_host, int32_t S);
+                          int64_t c_offset, const double* sos_host, int32_t S, uint64_t* key);
+int dsp_chain_status(void* workspace, size_t workspace_bytes, int32_t reset, void* stream);
+int64_t dsp_chain_spin_limit(int64_t spins);
 int dsp_chain_xstate_geometry(int64_t chunk_len, int32_t K, int32_t L, int32_t M,
                               int64_t c_offset, int64_t* shift, int64_t* q0,
                               int64_t* rows);
@@ -230,7 +254,8 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
                   int64_t c_offset, const double* sos_host, int32_t S,
                   int32_t clip, int64_t chunk_len, const double* state_table,
                   const double* xstate_table, int64_t xstate_rows,
-                  const void* tile_tables, int64_t seg_start, int64_t seg_len, int32_t log2n, int64_t ld_mag,
+                  const void* tile_tables, uint64_t tile_key, int64_t seg_start,
+                  int64_t seg_len, int32_t log2n, int64_t ld_mag,
                   const float* window, const float* twiddles, void* workspace,
                   size_t workspace_bytes, void* stream);
 

@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 25
+    assert len(names) == 27
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 10300
+    assert lib.dsp_version() == 20000     # 2.0.0: round 3 changed dsp_chain_f32's arguments
     assert isinstance(_lib.last_error(), str)
 
 
@@ -142,9 +142,9 @@ def test_chain_path_tile_len_and_workspace_query():
     """dsp_chain_path takes 0/1 (-1 queries); dsp_chain_tile_len names the
     single-pass geometries (config 3's L3/M2, K = 121: 48-sample sub-chunks;
     any L/M with ceil(K/L) <= 8, e.g. config 5's 160/147, K = 1023: 32) and
-    declines others; the chain workspace holds the tile hand-off (a 12-double
-    state and a flag per tile, 3072- or 2048-output tiles) or the two-launch
-    cascade's scratch, whichever is larger."""
+    declines others; the chain workspace holds a 256-byte status header, the
+    tile hand-off (a 12-double state and a flag per tile, 3072- or 2048-output
+    tiles) and, after it, the two-launch cascade's scratch (never shared)."""
     lib = _lib.load()
     prev = lib.dsp_chain_path(-1)
     assert prev in (0, 1)
@@ -163,15 +163,68 @@ def test_chain_path_tile_len_and_workspace_query():
     assert ws >= B * tiles * (12 * 8 + 4)
     assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 1023, 160, 147, 511, 6, 1152) >= \
         B * -(-52245 // 2048) * (12 * 8 + 4)
-    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 6401, 160, 147, 3200, 6, 1152) == 0
+    # no single-pass kernel and a fused cascade: the status header alone
+    assert lib.dsp_chain_workspace_bytes(B, n_in, 52245, 6401, 160, 147, 3200, 6, 1152) == 256
+    # the two-launch cascade's scratch (282 chunks: general path) follows the hand-off region
+    head = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)
+    assert lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 256) == \
+        head + lib.dsp_biquad_workspace_bytes(B, n_out, 6, 256)
+
+
+def test_chain_status_spin_limit_and_null_y_validation():
+    """dsp_chain_spin_limit is per thread (default 2^23 polls, -1 queries);
+    dsp_chain_status rejects a null workspace; y == NULL is refused where the
+    single-pass kernel does not serve the call (no tables), before any launch."""
+    import threading
+    lib = _lib.load()
+    assert _lib.spin_limit() == 1 << 23
+    assert _lib.spin_limit(0) == 1 << 23 and _lib.spin_limit() == 0
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(_lib.spin_limit()))
+    t.start()
+    t.join()
+    assert seen == [1 << 23]                       # another thread keeps the default
+    assert _lib.spin_limit(1 << 23) == 0
+    assert lib.dsp_chain_spin_limit(-2) == _lib.DSP_EINVAL
+    assert lib.dsp_chain_status(None, 0, 0, None) == _lib.DSP_EINVAL
+    ws = lib.dsp_chain_workspace_bytes(1, 48000, 72000, 121, 3, 2, 60, 6, 1152)
+    rc = lib.dsp_chain_f32(16, None, 32, 48, 1, 48000, 48000, 72000, 72000, 64, 121, 3, 2, 60,
+                           None, 0, 0, 1152, None, None, 0, None, 0, 0, 2048, 11, 1025, 80, 96,
+                           112, ws, None)
+    assert rc == _lib.DSP_EINVAL and "NULL" in _lib.last_error()
+    rc = lib.dsp_chain_f32(16, None, 32, 48, 1, 48000, 48000, 72000, 72000, 64, 121, 3, 2, 60,
+                           None, 0, 0, 1152, None, None, 0, None, 0, 0, 2048, 11, 1025, 80, 96,
+                           112, 16, None)
+    assert rc == _lib.DSP_EINVAL and "workspace" in _lib.last_error()
+
+
+def _tables_dtype():
+    """numpy mirror of csrc/chain_tile.hip's TileTables (C layout)."""
+    import numpy as np
+    return np.dtype([("key", "<u8"), ("G", "<f8", (64, 12)), ("Gc", "<f4", (32, 12, 2)),
+                     ("Q", "<f8", (12, 12)), ("Dp", "<f8", (6, 6, 2, 2)), ("T", "<f8", (12, 12)),
+                     ("TP", "<f4", (32, 4, 2)), ("geo", "<i4", (6,)), ("cf", "<f8", (6, 4)),
+                     ("gain", "<f8"), ("seq", "<f4", (8, 32, 8)), ("adv", "<u4", (8,)),
+                     ("classes", "<i4"), ("pad", "<i4"), ("seqs", "<f4", (8, 32, 12))], align=True)
+
+
+def _tables(lib, nbytes, *args):
+    import numpy as np
+    buf = np.zeros(nbytes, np.uint8)
+    key = ctypes.c_uint64(0)
+    rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, *args, ctypes.byref(key))
+    return rc, buf.view(_tables_dtype())[0], key.value
 
 
 def test_chain_tile_tables_host_only():
     """dsp_chain_tile_tables (host, no GPU) for config 3's geometry: the
     block-diagonal carry tables reproduce the cascade's dense state algebra
     (T D^(48 2^d) T^-1 = A^(48 2^d); T sum_i G'[i] y[i] = the zero-state end
-    state of a 48-sample sub-chunk) and the tap pairs are the reversed
-    polyphase branches shifted by their window parity; config 5's geometry
+    state of a 48-sample sub-chunk); the float32 pass-1 rows in input-normal
+    coordinates give the same end state through Q (T Q sum_i Gc[i] y[i]), Q is
+    lower triangular and the coordinates have unit variance under white noise;
+    the tap pairs are the reversed polyphase branches shifted by their window
+    parity; the key fingerprints geometry and cascade; config 5's geometry
     builds 32-sample tables for the generic kernel; others decline with 1."""
     import numpy as np
 
@@ -182,23 +235,18 @@ def test_chain_tile_tables_host_only():
     plan = design.src_plan(48000, 48000, 2, 3)
     sos = np.ascontiguousarray(design.eq_plan(72000, gains).sos)
     nbytes = lib.dsp_chain_tile_tables_bytes()
-    assert nbytes == (64 * 12 * 8 + 6 * 6 * 4 * 8 + 144 * 8 + 32 * 4 * 2 * 4 + 6 * 4 + 6 * 4 * 8 + 8
-                      + 8 * 32 * 8 * 4 + 8 * 4 + 2 * 4 + 8 + 8 * 32 * 12 * 4)   # 8: 16-B alignment
-    buf = np.zeros(nbytes, np.uint8)
+    assert nbytes == _tables_dtype().itemsize
     taps32 = np.ascontiguousarray(plan.taps, dtype=np.float32)
-    rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, 72000, taps32.ctypes.data,
-                                   plan.K, 3, 2, plan.c_offset, _lib.sos_pointer(sos), 6)
-    assert rc == 0
-    G = buf[:6144].view(np.float64).reshape(64, 12)
-    Dp = buf[6144:7296].view(np.float64).reshape(6, 6, 2, 2)
-    T = buf[7296:8448].view(np.float64).reshape(12, 12)
-    TP = buf[8448:9472].view(np.float32).reshape(32, 4, 2)
-    assert tuple(buf[9472:9496].view(np.int32)) == (48, 21, 3, 2, 121, 6)
+    rc, tb, key = _tables(lib, nbytes, 48000, 72000, taps32.ctypes.data, plan.K, 3, 2,
+                          plan.c_offset, _lib.sos_pointer(sos), 6)
+    assert rc == 0 and key != 0 and int(tb["key"]) == key
+    G, Dp, T, TP = tb["G"], tb["Dp"], tb["T"], tb["TP"]
+    assert tuple(tb["geo"]) == (48, 21, 3, 2, 121, 6)
     # the DF2 realisation pass 2 reads: per stage {b1/b0, b2/b0, a1, a2}, gain prod(b0)
     rows, gain, norm = design.df2_realization(sos)
     assert norm
-    np.testing.assert_array_equal(buf[9496:9688].view(np.float64).reshape(6, 4), rows[:, 1:])
-    assert buf[9688:9696].view(np.float64)[0] == gain
+    np.testing.assert_array_equal(tb["cf"], rows[:, 1:])
+    assert tb["gain"] == gain
     A, B = design.state_space(sos)
     Ti = np.linalg.inv(T)
     for d in range(6):
@@ -207,11 +255,30 @@ def test_chain_tile_tables_host_only():
             D[2 * k:2 * k + 2, 2 * k:2 * k + 2] = Dp[d, k]
         An = np.linalg.matrix_power(A, 48 << d)
         np.testing.assert_allclose(T @ D @ Ti, An, atol=1e-9 * max(1.0, np.abs(An).max()))
-    y = np.random.default_rng(0).uniform(-1, 1, 48)
+    y = np.random.default_rng(0).uniform(-1, 1, 48).astype(np.float32)
     X = np.zeros(12)
     for v in y:
-        X = A @ X + B * v
+        X = A @ X + B * float(v)
     np.testing.assert_allclose(T @ (G[:48].T @ y), X, rtol=1e-10, atol=1e-12)
+    # input-normal pass 1: float32 rows, Q = T^-1 P lower triangular
+    Q = tb["Q"]
+    Gc = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)   # rows 2j, 2j+1
+    assert np.array_equal(Q, np.tril(Q)) and not Gc[48:].any()
+    np.testing.assert_allclose(T @ (Q @ (Gc[:48].T @ y)), X, rtol=1e-5, atol=1e-6 * np.abs(X).max())
+    P = T @ Q                                   # DF2 coordinates = P * input-normal ones
+    W = np.zeros((12, 12))                      # state covariance, unit white noise
+    g = B.copy()
+    for _ in range(60000):
+        W += np.outer(g, g)
+        g = A @ g
+    np.testing.assert_allclose(np.linalg.solve(P, np.linalg.solve(P, W).T), np.eye(12), atol=1e-5)
+    # the key follows the cascade and the geometry
+    sos2 = sos.copy()
+    sos2[0, 0] *= 1 + 1e-15
+    assert _tables(lib, nbytes, 48000, 72000, taps32.ctypes.data, plan.K, 3, 2, plan.c_offset,
+                   _lib.sos_pointer(np.ascontiguousarray(sos2)), 6)[2] not in (0, key)
+    assert _tables(lib, nbytes, 48008, 72012, taps32.ctypes.data, plan.K, 3, 2, plan.c_offset,
+                   _lib.sos_pointer(sos), 6)[2] not in (0, key)
     # tap pairs: branch ph, pair p = (h[2p - a], h[2p + 1 - a]), h[u] = taps[ph + 3 (40 - u)]
     for ph in range(3):
         a = [((2 * i) // 3) & 1 for i in range(48) if (2 * i) % 3 == ph][0]
@@ -225,23 +292,23 @@ def test_chain_tile_tables_host_only():
     # config 5 (generic kernel): 32-sample sub-chunks, no tap pairs (the kernel
     # reads the device taps); 41 taps per branch declines with 1.
     sos5 = np.ascontiguousarray(design.eq_plan(c5.fs_out, gains).sos)
-    buf[:] = 0
-    assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c5.n_out, t5.ctypes.data,
-                                     c5.K, 160, 147, c5.c_offset, _lib.sos_pointer(sos5), 6) == 0
-    assert tuple(buf[9472:9496].view(np.int32)) == (32, 0, 160, 147, 1023, 6)
-    G5 = buf[:6144].view(np.float64).reshape(64, 12)
-    T5 = buf[7296:8448].view(np.float64).reshape(12, 12)
+    rc, tb, key5 = _tables(lib, nbytes, 48000, c5.n_out, t5.ctypes.data, c5.K, 160, 147,
+                           c5.c_offset, _lib.sos_pointer(sos5), 6)
+    assert rc == 0 and key5 not in (0, key)
+    assert tuple(tb["geo"]) == (32, 0, 160, 147, 1023, 6)
     A5, B5 = design.state_space(sos5)
-    y = np.random.default_rng(1).uniform(-1, 1, 32)
+    y = np.random.default_rng(1).uniform(-1, 1, 32).astype(np.float32)
     X = np.zeros(12)
     for v in y:
-        X = A5 @ X + B5 * v
-    np.testing.assert_allclose(T5 @ (G5[:32].T @ y), X, rtol=1e-10, atol=1e-12)
-    assert not buf[8448:9472].any()
+        X = A5 @ X + B5 * float(v)
+    np.testing.assert_allclose(tb["T"] @ (tb["G"][:32].T @ y), X, rtol=1e-10, atol=1e-12)
+    Gc5 = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)
+    np.testing.assert_allclose(tb["T"] @ (tb["Q"] @ (Gc5[:32].T @ y)), X,
+                               rtol=1e-5, atol=1e-6 * np.abs(X).max())
+    assert not tb["TP"].any()
     # class tables: sub-chunks start at outputs 32 j; class j mod 5 (32*147 mod 160 = 64)
-    seq = buf[9696:9696 + 8192].view(np.float32).reshape(8, 32, 8)
-    adv = buf[17888:17920].view(np.uint32)
-    assert tuple(buf[17920:17928].view(np.int32))[0] == 5
+    seq, adv = tb["seq"], tb["adv"]
+    assert tb["classes"] == 5
     L, M, K, c = 160, 147, 1023, c5.c_offset
     for k in range(5):
         phi = (c + k * 64) % L
@@ -254,7 +321,7 @@ def test_chain_tile_tables_host_only():
     # k_chain_gct's rows: output i reads window pairs from (i M div L) rounded
     # down to even; its T = 7 taps sit shifted by (i M div L) mod 2 + the
     # class's carry d_i in 10 of 12 slots
-    seqs = buf[17936:17936 + 12288].view(np.float32).reshape(8, 32, 12)
+    seqs = tb["seqs"]
     for k in range(5):
         phi0 = (c + k * 64) % L
         for i in range(32):
@@ -268,5 +335,6 @@ def test_chain_tile_tables_host_only():
     assert not seqs[5:].any()
     c6 = design.src_plan(48000, 44100, 147, 160)
     t6 = np.ascontiguousarray(c6.taps, dtype=np.float32)
-    assert lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, c6.n_out, t6.ctypes.data,
-                                     c6.K, 160, 147, c6.c_offset, _lib.sos_pointer(sos5), 6) == 1
+    rc, _, key6 = _tables(lib, nbytes, 48000, c6.n_out, t6.ctypes.data, c6.K, 160, 147,
+                          c6.c_offset, _lib.sos_pointer(sos5), 6)
+    assert rc == 1 and key6 == 0

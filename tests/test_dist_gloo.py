@@ -70,3 +70,44 @@ def test_timed_loop_preheat_then_exact_counts():
     elapsed = bench.timed_loop(step, steps=3, warmup=2, sync=lambda: None, preheat_s=0.03)
     assert len(calls) >= 2 + 3 + 10          # >= 30 ms of 2 ms pre-heat steps
     assert 0.005 <= elapsed < 0.05           # only the 3 timed steps
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(DSP_BENCH_DRYRUN="1", **extra)
+    return env
+
+
+def test_bench_gpus_flag_launches_the_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher starts two ranks (fresh
+    processes, gloo rendezvous on 127.0.0.1) that shard config 4's 32768
+    channels (0, 16384) and (16384, 32768); rank 0 alone prints the line.
+    DSP_BENCH_DRYRUN stubs the GPU measurement (measure_stub)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--steps", "3", "--warmup", "1"], capture_output=True, text=True,
+                         timeout=300, env=_bench_env(), cwd=root)
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3
+    assert out["config"]["total_channels"] == 32768
+    assert out["config"]["channels_per_gpu"] == 16384
+    assert out["config"]["parallelism"] == "channel-shard x2 (no collective)"
+    assert out["cpu_baseline"] is None                  # N > 1: rank 0 skips the CPU leg
+
+
+def test_bench_refuses_gpus_other_than_world_size():
+    """Under a launcher, --gpus must equal WORLD_SIZE (one rank per GPU)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4",
+                          "--steps", "1"], capture_output=True, text=True, timeout=120,
+                         env=_bench_env(RANK="0", LOCAL_RANK="0", WORLD_SIZE="2"), cwd=root)
+    assert res.returncode != 0 and "WORLD_SIZE=2" in res.stderr

@@ -8,8 +8,8 @@ survey container):
     length bit-exact (delta inputs reproduce float32(L*h[k]) exactly);
   * EQ: float64 coefficients and state, float32 I/O -> atol 1e-5;
   * FFT: float32 with float64-computed twiddles -> max|dX| <= 1e-5 * max|X|;
-  * chain spectrum: the EQ tolerance propagated through the window and FFT ->
-    max|dmag| <= 1e-4 * max|mag|.
+  * chain spectrum: the FFT tolerance, max|dmag| <= 1e-5 * max|mag| (observed
+    3.5e-7 on the smoke case; round 2 allowed 1e-4).
 """
 import contextlib
 
@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 SRC_ATOL = 2e-6
 EQ_ATOL = 1e-5
 FFT_RTOL = 1e-5
-CHAIN_MAG_RTOL = 1e-4
+CHAIN_MAG_RTOL = 1e-5
 
 
 def _dc():

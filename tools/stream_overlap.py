@@ -28,7 +28,7 @@ def run(nstreams):
     for i in range(K):
         s = streams[i % nstreams] if nstreams > 1 else torch.cuda.current_stream(dev)
         with torch.cuda.stream(s):
-            chains[i % 2].run(x)
+            chains[i % 2].run(x, check=False)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / K * 1e3
 
