@@ -167,7 +167,7 @@ size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t
   // the two paths never share bytes, so switching paths (dsp_chain_path, or a
   // geometry the single-pass kernel declines) cannot leave stale hand-off flags.
   const size_t head = dsp::chain_tile_workspace_bytes(B, n_in, n_out, K, L, M, c_offset, S);
-  return head + dsp::biquad_workspace_bytes(B, n_out, S, chunk_len);
+  return dsp::add_sat(head, dsp::biquad_workspace_bytes(B, n_out, S, chunk_len));
 }
 
 int dsp_chain_status(void* workspace, size_t workspace_bytes, int32_t reset, void* stream) {

@@ -225,6 +225,7 @@ int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
   }
   DSP_REQUIRE(have_fmt && w.data_offset > 0, "no fmt/data chunk");
   DSP_REQUIRE(w.channels >= 1 && w.channels <= 128, "channels=%d outside [1, 128]", w.channels);
+  DSP_REQUIRE(w.sample_rate > 0, "sample rate %d", w.sample_rate);
   if (tag == 1) {
     w.format = DSP_WAV_PCM;
     DSP_REQUIRE(w.bits == 8 || w.bits == 16 || w.bits == 24 || w.bits == 32,
@@ -241,9 +242,12 @@ int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
 }
 
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames) {
-  DSP_REQUIRE(out && fs > 0 && channels >= 1 && frames >= 0, "bad header arguments");
+  DSP_REQUIRE(out && fs > 0 && channels >= 1 && channels <= 65535 && frames >= 0,
+              "bad header arguments");
+  DSP_REQUIRE(frames <= ((int64_t)UINT32_MAX - 36) / (2 * (int64_t)channels),
+              "data too large for RIFF");
+  DSP_REQUIRE((int64_t)fs * channels * 2 <= (int64_t)UINT32_MAX, "byte rate too large for RIFF");
   const int64_t data = frames * channels * 2;
-  DSP_REQUIRE(data + 36 <= (int64_t)UINT32_MAX, "data too large for RIFF");
   memcpy(out, "RIFF", 4);
   wr32(out + 4, (uint32_t)(36 + data));
   memcpy(out + 8, "WAVEfmt ", 8);
@@ -251,7 +255,7 @@ int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames)
   wr16(out + 20, 1);
   wr16(out + 22, (uint16_t)channels);
   wr32(out + 24, (uint32_t)fs);
-  wr32(out + 28, (uint32_t)(fs * channels * 2));
+  wr32(out + 28, (uint32_t)((int64_t)fs * channels * 2));
   wr16(out + 32, (uint16_t)(channels * 2));
   wr16(out + 34, 16);
   memcpy(out + 36, "data", 4);

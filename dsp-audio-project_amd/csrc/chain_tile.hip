@@ -886,7 +886,7 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
   return false;
 }
 
-size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+size_t align256(size_t v) { return v > SIZE_MAX - 255 ? SIZE_MAX : (v + 255) & ~(size_t)255; }
 
 // Fingerprint of everything the tables depend on that a call can state on the
 // host: the kernel kind and geometry, the cascade (sos bits) and the table
@@ -1202,8 +1202,10 @@ TileWs tile_ws(int64_t B, int64_t ntiles) {
   TileWs w;
   w.err_off = 0;  // include/dspcore.h: the workspace's first word
   w.st_off = 256;
-  w.fl_off = w.st_off + align256((size_t)B * ntiles * kD * sizeof(double));
-  w.total = w.fl_off + align256((size_t)B * ntiles * sizeof(uint32_t));
+  const size_t st = mul_sat((size_t)B, (size_t)ntiles, kD, sizeof(double));
+  const size_t fl = mul_sat((size_t)B, (size_t)ntiles, sizeof(uint32_t));
+  w.fl_off = st == SIZE_MAX ? SIZE_MAX : add_sat(w.st_off, align256(st));
+  w.total = (fl == SIZE_MAX || w.fl_off == SIZE_MAX) ? SIZE_MAX : add_sat(w.fl_off, align256(fl));
   return w;
 }
 

@@ -57,6 +57,17 @@ class TraceScope {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// a * b * c * d in size_t, saturating at SIZE_MAX (a workspace nobody can
+// allocate: the launch then fails its size check instead of wrapping).
+inline size_t mul_sat(size_t a, size_t b, size_t c = 1, size_t d = 1) {
+  size_t r;
+  if (__builtin_mul_overflow(a, b, &r) || __builtin_mul_overflow(r, c, &r) ||
+      __builtin_mul_overflow(r, d, &r))
+    return SIZE_MAX;
+  return r;
+}
+inline size_t add_sat(size_t a, size_t b) { return a > SIZE_MAX - b ? SIZE_MAX : a + b; }
+
 // Dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB).
 template <typename Kern>
 inline int allow_lds(Kern kernel, size_t bytes) {

@@ -654,7 +654,7 @@ int dispatch(const FftArgs& a, int log2n, hipStream_t s) {
 
 size_t fft_workspace_bytes(int64_t B, int log2n) {
   if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
-  return (size_t)B * ((size_t)1 << log2n) * sizeof(float2);
+  return mul_sat((size_t)B, (size_t)1 << log2n, sizeof(float2));
 }
 
 namespace {

@@ -627,7 +627,7 @@ __global__ __launch_bounds__(1024) void k_iir_prep(SosParams p, int S, int64_t T
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+size_t align256(size_t v) { return v > SIZE_MAX - 255 ? SIZE_MAX : (v + 255) & ~(size_t)255; }
 
 struct WsLayout {
   size_t p_off, e_off, s_off, total;
@@ -644,8 +644,14 @@ WsLayout ws_layout(int64_t B, int64_t n, int S, int64_t T) {
   const size_t D = 2 * (size_t)S;
   w.p_off = 0;
   w.e_off = align256(D * D * sizeof(double));
-  w.s_off = w.e_off + align256((size_t)B * (C - 1) * D * sizeof(double));
-  w.total = w.s_off + align256((size_t)B * C * D * sizeof(double));
+  const size_t e_bytes = mul_sat((size_t)B, (size_t)(C - 1), D, sizeof(double));
+  const size_t s_bytes = mul_sat((size_t)B, (size_t)C, D, sizeof(double));
+  if (e_bytes == SIZE_MAX || s_bytes == SIZE_MAX) {
+    w.total = SIZE_MAX;
+    return w;
+  }
+  w.s_off = add_sat(w.e_off, align256(e_bytes));
+  w.total = add_sat(w.s_off, align256(s_bytes));
   return w;
 }
 
@@ -765,6 +771,9 @@ int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
                     int64_t* q0, int64_t* rows) {
   DSP_REQUIRE(chunk_len > 0 && K >= 1 && L >= 1 && M >= 1 && c >= 0, "bad SRC/chunk geometry");
+  DSP_REQUIRE(chunk_len <= ((int64_t)1 << 40) && L <= (1 << 24) && M <= (1 << 24) &&
+                  c <= ((int64_t)1 << 40),
+              "SRC/chunk geometry out of range");
   DSP_REQUIRE((chunk_len * M) % L == 0, "chunk_len*M=%lld is not a multiple of L=%d",
               (long long)(chunk_len * M), L);
   const int64_t sh = chunk_len * M / L;

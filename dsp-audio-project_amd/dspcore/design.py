@@ -156,6 +156,62 @@ def tf_to_sos_row(b, a) -> np.ndarray:
     return np.array([bb[0], bb[1], bb[2], aa[1], aa[2]])
 
 
+@dataclass(frozen=True)
+class LfilterPlan:
+    """How aplicar_ecuacion_diferencias runs lfilter(b, a, x) of any order
+    (reference dsp_core.py:205-214): 'sos' -- the transfer function as
+    second-order sections (float64, host) for the biquad-cascade kernel;
+    'fir' -- a pure FIR (a == [1] after normalisation, more than 3 taps) as a
+    causal convolution on the SRC kernel with L = M = 1; 'gain' -- b and a of
+    length 1 (y = b0/a0 x)."""
+    kind: str
+    sos: np.ndarray | None = None
+    taps: np.ndarray | None = None
+    gain: float = 1.0
+
+
+MAX_LFILTER_SECTIONS = 16     # include/dspcore.h DSP_MAX_STAGES: IIR orders up to 32
+
+
+def lfilter_plan(b, a) -> LfilterPlan:
+    """Plan of scipy.signal.lfilter(b, a, x) for 1-D b, a of any length.
+
+    Like lfilter, every coefficient is divided by a[0] (a[0] == 0 raises the
+    ValueError lfilter raises).  Orders <= 2 keep the direct biquad row; higher
+    IIR orders are factored into second-order sections with
+    scipy.signal.tf2sos (poles and zeros in float64; the cascade is the same
+    transfer function as lfilter's direct form II transposed, and better
+    conditioned); IIR orders above 2 * DSP_MAX_STAGES raise RuntimeError.
+    """
+    b = np.atleast_1d(np.asarray(b, dtype=np.float64))
+    a = np.atleast_1d(np.asarray(a, dtype=np.float64))
+    if b.ndim != 1 or a.ndim != 1 or b.size == 0 or a.size == 0:
+        raise ValueError("b and a must be non-empty 1-D coefficient vectors")
+    if a[0] == 0:
+        raise ValueError("BUG: filter coefficient a[0] == 0 not supported yet")
+    b = b / a[0]
+    a = a / a[0]
+    a_tail = np.trim_zeros(a[1:], "b")
+    if a_tail.size == 0:
+        if b.size == 1:
+            return LfilterPlan("gain", gain=float(b[0]))
+        if b.size > 3:
+            return LfilterPlan("fir", taps=b.copy())
+    if max(a.size, b.size) <= 3:
+        return LfilterPlan("sos", sos=tf_to_sos_row(b, a).reshape(1, 5))
+    import scipy.signal
+    a = np.concatenate([[1.0], a_tail])
+    sos6 = scipy.signal.tf2sos(b, a)            # rows b0 b1 b2 a0(=1) a1 a2
+    if sos6.shape[0] > MAX_LFILTER_SECTIONS:
+        raise RuntimeError(
+            f"aplicar_ecuacion_diferencias: order {max(a.size, b.size) - 1} needs "
+            f"{sos6.shape[0]} second-order sections; the GPU cascade takes at most "
+            f"{MAX_LFILTER_SECTIONS}")
+    sos = np.ascontiguousarray(np.column_stack([sos6[:, 0:3] / sos6[:, 3:4],
+                                                sos6[:, 4:6] / sos6[:, 3:4]]))
+    return LfilterPlan("sos", sos=sos)
+
+
 MAX_FUSED_CHUNKS = 256   # csrc/iir.hip kCBMax: four waves of 64 chunk lanes per channel
 WIDE_BATCH = 2048        # from this many channels one wave (<= 64 chunks) per channel fills the chip
 

@@ -205,11 +205,26 @@ def disenar_coeficientes_diferencias(fc, fs, ganancia_db):
 
 
 def aplicar_ecuacion_diferencias(x_n, b, a):
-    """y = lfilter(b, a, x) for a biquad (dsp_core.py:205-214), zero initial state."""
-    row = _design.tf_to_sos_row(b, a)
+    """y = lfilter(b, a, x), zero initial state (dsp_core.py:205-214), any order.
+
+    Biquads and second-order sections of higher IIR orders (design.lfilter_plan,
+    float64 on the host) run on the float64 biquad-cascade kernel; a pure FIR
+    longer than 3 taps runs as a causal convolution on the SRC kernel (L = M =
+    1, float32 taps and sums); b/a of length 1 is a gain.  a[0] == 0 raises
+    ValueError as lfilter does.
+    """
+    plan = _design.lfilter_plan(b, a)
     ops = _ops()
     t, how = _to_rows(x_n)
-    y = ops.biquad_cascade(t, row.reshape(1, 5), clip=False)
+    if plan.kind == "fir":
+        n = int(t.shape[1])
+        src = _design.SrcPlan(1, 1, int(plan.taps.size), plan.taps, 0, n, n, 0)
+        y = ops.src_polyphase(t, src)
+    elif plan.kind == "gain":
+        # one exact-product pass: the cascade kernel with the gain as b0
+        y = ops.biquad_cascade(t, np.array([[plan.gain, 0.0, 0.0, 0.0, 0.0]]), clip=False)
+    else:
+        y = ops.biquad_cascade(t, plan.sos, clip=False)
     return _from_rows(y, how, np.float64)
 
 

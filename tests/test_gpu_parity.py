@@ -163,6 +163,28 @@ def test_single_biquad_matches_lfilter(gpu):
         assert np.max(np.abs(y - scipy.signal.lfilter(b, a, x))) <= EQ_ATOL
 
 
+def test_difference_equation_any_order_matches_lfilter(gpu):
+    """aplicar_ecuacion_diferencias for any (b, a), as lfilter takes them
+    (reference dsp_core.py:214): orders 1-8 (Butterworth, Chebyshev, elliptic,
+    random stable), b longer than a, a[0] != 1, FIRs, a pure gain -- within
+    1e-5 of scipy.signal.lfilter (relative to max|y| when that exceeds 1), 1-D
+    numpy in -> float64 out, 2-D batches per row."""
+    import scipy.signal
+    from test_host_logic import _lfilter_cases
+    dc = _dc()
+    x = np.random.default_rng(5).uniform(-1, 1, (2, 20000))
+    for name, b, a in _lfilter_cases():
+        ref = scipy.signal.lfilter(b, a, x[0])
+        y = dc.aplicar_ecuacion_diferencias(x[0], b, a)
+        assert y.dtype == np.float64 and y.shape == ref.shape
+        err = np.max(np.abs(y - ref))
+        assert err <= EQ_ATOL * max(1.0, np.max(np.abs(ref))), (name, err)
+        yb = dc.aplicar_ecuacion_diferencias(x, b, a)
+        np.testing.assert_array_equal(yb[0], y)
+    with pytest.raises(ValueError):
+        dc.aplicar_ecuacion_diferencias(x[0], [1.0], [0.0, 1.0])
+
+
 def test_eq_chunk_carry_is_exact_to_rounding(gpu):
     """Every scan variant vs one chunk per channel (a plain serial recursion),
     at config-3 length: fused kernel with / without the state-response table,

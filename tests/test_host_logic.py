@@ -206,3 +206,51 @@ def test_bluestein_tables_compute_the_dft():
         d = np.fft.fft(np.conj(np.fft.fft(a) * bf))
         got = chirp * np.conj(d[:n])
         assert np.max(np.abs(got - np.fft.fft(x))) <= 1e-12 * max(1.0, np.max(np.abs(got)))
+
+
+def _lfilter_cases():
+    import scipy.signal as ss
+    rng = np.random.default_rng(12)
+    poles = 0.9 * np.sqrt(rng.uniform(0, 1, 3)) * np.exp(1j * rng.uniform(0, np.pi, 3))
+    a_rand = np.real(np.poly(np.concatenate([poles, np.conj(poles), [0.5]])))
+    return [
+        ("order 1", [0.5, 0.5], [1.0, -0.3]),
+        ("biquad, a0 = 2", [1.0, -1.2, 0.5], [2.0, -1.0, 0.4]),
+        ("butter 3 lp", *ss.butter(3, 0.2)),
+        ("butter 4 hp", *ss.butter(4, 0.3, "highpass")),
+        ("butter 4 bp (order 8)", *ss.butter(4, [0.2, 0.4], "bandpass")),
+        ("butter 8 lp", *ss.butter(8, 0.4)),
+        ("cheby1 5", *ss.cheby1(5, 1, 0.3)),
+        ("ellip 6", *ss.ellip(6, 0.5, 40, 0.35)),
+        ("random stable order 7", rng.uniform(-1, 1, 8), a_rand),
+        ("b longer than a", [0.2, 0.3, -0.1, 0.05, 0.4, 0.1], [1.0, -0.5, 0.2]),
+        ("fir 31", ss.firwin(31, 0.2), [1.0]),
+        ("fir 5, a = [2]", [1.0, 2.0, 3.0, 2.0, 1.0], [2.0]),
+        ("gain", [3.0], [4.0]),
+    ]
+
+
+def test_lfilter_plan_any_order_matches_lfilter():
+    """design.lfilter_plan (aplicar_ecuacion_diferencias, any order): the
+    second-order sections it hands the cascade kernel filter exactly like
+    scipy.signal.lfilter (checked in float64 with sosfilt), the FIR and gain
+    plans are lfilter's normalised b; a[0] == 0 raises lfilter's ValueError."""
+    import scipy.signal as ss
+    from dspcore import design
+    x = np.random.default_rng(3).uniform(-1, 1, 4000)
+    for name, b, a in _lfilter_cases():
+        ref = ss.lfilter(b, a, x)
+        plan = design.lfilter_plan(b, a)
+        if plan.kind == "sos":
+            sos6 = np.column_stack([plan.sos[:, :3], np.ones(plan.sos.shape[0]), plan.sos[:, 3:]])
+            got = ss.sosfilt(sos6, x)
+            assert plan.sos.shape[0] <= design.MAX_LFILTER_SECTIONS
+        elif plan.kind == "fir":
+            got = np.convolve(x, plan.taps)[:x.size]
+        else:
+            got = plan.gain * x
+        assert np.max(np.abs(got - ref)) <= 1e-9 * max(1.0, np.max(np.abs(ref))), name
+    with pytest.raises(ValueError, match="a\\[0\\] == 0"):
+        design.lfilter_plan([1.0], [0.0, 1.0])
+    with pytest.raises(RuntimeError, match="sections"):
+        design.lfilter_plan([1.0], np.poly(0.5 * np.ones(34)))

@@ -1,0 +1,36 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (SURVEY.md §5:
+race detection / sanitizers on the host C++).
+
+`make -C dsp-audio-project_amd/csrc sanitize` builds the library's sources with
+-fsanitize=address,undefined on the host side (-Xarch_host; device code is
+compiled normally and never launched) and links tests/native/host_fuzz.cpp,
+which feeds the host entry points a malformed-input corpus: every truncation
+and byte/size-field corruption of valid WAV headers, nonsense fmt fields and
+random bytes into dsp_wav_parse (exact-size heap buffers: any over-read is an
+ASan report), extreme arguments into the playback header writer, and edge
+geometries / cascades into the chain planners (tile tables, tile length,
+workspace sizes, x-state geometry, Bluestein and FFT sizes).  No GPU needed.
+__graft_entry__.build() builds the binary; this test builds it if missing.
+"""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dsp-audio-project_amd", "csrc")
+BIN = os.path.join(ROOT, "dsp-audio-project_amd", "build", "asan", "host_fuzz")
+
+
+def test_host_entry_points_under_asan_ubsan():
+    jobs = str(min(8, os.cpu_count() or 1))
+    build = subprocess.run(["make", "-C", CSRC, f"-j{jobs}", "sanitize"], capture_output=True,
+                           text=True, timeout=1500)
+    assert build.returncode == 0, build.stdout[-3000:] + build.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    res = subprocess.run([BIN], capture_output=True, text=True, timeout=900, env=env)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    assert "runtime error" not in out and "AddressSanitizer" not in out, out[-4000:]
+    assert "0 failures" in out
+    parsed = int(out.split("host_fuzz: ")[1].split(" parsed")[0])
+    assert parsed > 1000                      # the corpus reaches the success path too
