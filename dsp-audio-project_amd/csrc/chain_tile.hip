@@ -54,17 +54,25 @@
 // chip's resident wave count its end state is normally published long before
 // tile t needs it.  A workgroup waits only on a lower id, and ids are
 // dispatched in order, so every wait ends.  The state (12 doubles) and its
-// flag are an agent-scope release/acquire pair: the producer lane stores the
-// payload (sc1), fences (release, agent: buffer_wbl2 sc1 + vmcnt(0)) and stores
-// the flag; the consumer polls the flag (relaxed, sc1), fences (acquire,
-// agent: buffer_inv sc1) and loads the payload.  The consumer clears the flag,
-// so a completed launch leaves the flag array zero for the next one (the
-// caller zero-fills the workspace once).  A wait that polls more than the
-// thread's spin limit (dsp_chain_spin_limit; default 2^23 polls with
-// s_sleep 2 between them, ~0.4 s: a broken dispatch order, or a GPU
-// time-sliced between processes) gives up: it sets the workspace's status word
-// (dsp_chain_status reports it, Chain.run raises) and leaves the flag for the
-// workspace reset; z of that launch is wrong, nothing hangs.
+// flag are agent-scope atomics (global loads/stores with sc1: coherent at
+// device scope across the XCDs' L2s, per location).  The producer lane stores
+// the payload, waits vmcnt(0) (every payload store acknowledged) and only then
+// stores the flag; the consumer polls the flag and issues the payload loads
+// only after a poll returned 1 (a control dependency on a returned value, and
+// asm memory clobbers keep the compiler from hoisting them).  Ordering between
+// the payload and the flag therefore rests on the gfx950 ISA, not on C++
+// release/acquire: the memory model's agent-scope release/acquire fences add
+// buffer_wbl2 sc1 / buffer_inv sc1 (L2 write-back / invalidate), which the
+// atomics do not need and which measured 5.8x slower (config 4: 37.7 vs
+// 6.55 ms, profiles/r03_handoff_fence_ab.txt; -DDSP_HANDOFF_FENCED=1 builds
+// that variant).  The consumer clears the flag, so a completed launch leaves
+// the flag array zero for the next one (the caller zero-fills the workspace
+// once).  A wait that polls more than the thread's spin limit
+// (dsp_chain_spin_limit; default 2^23 polls with s_sleep 2 between them,
+// ~0.4 s: a broken dispatch order, or a GPU time-sliced between processes)
+// gives up: it sets the workspace's status word (dsp_chain_status reports it,
+// Chain.run raises) and leaves the flag for the workspace reset; z of that
+// launch is wrong, nothing hangs.
 //
 // Rows are bitwise independent of the batch size: the geometry depends on
 // (L, M, K) only.
@@ -409,7 +417,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       }
       __builtin_amdgcn_s_sleep(2);
     }
-#if !DSP_HANDOFF_RELAXED
+#if DSP_HANDOFF_FENCED
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
     fence();
@@ -456,10 +464,10 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     const int64_t me = b * a.ntiles + tile;
 #pragma unroll
     for (int d = 0; d < kD; ++d) store_state(a.states + me * kD + d, v[d]);
-#if DSP_HANDOFF_RELAXED
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
+#if DSP_HANDOFF_FENCED
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     store_flag(a.flags + me, 1u);
   }

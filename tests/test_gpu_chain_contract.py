@@ -99,7 +99,7 @@ def test_config1_chain_two_launch_bypass(gpu):
     assert ch.tile_len == 0 and ch.eq.bypass and ch.sos.shape[0] == 0
     xs = torch.from_numpy(np.stack([x, -x])).to(gpu)
     (y, z, mag), names = _traced(lambda: ch.run(xs))
-    assert names == ["src_poly", "iir_fused", "spectrum"], names
+    assert names == ["src_poly", "iir_apply", "spectrum"], names   # S = 0: one copy pass
     assert torch.equal(y, z)
     ry, rz, _, rm, _ = orc.chain(x, fs, 2, 1, FLAT, 127, 1024, limit_pts=100000)
     y, mag = y.cpu().numpy(), mag.cpu().numpy()
