@@ -37,6 +37,8 @@ namespace {
 
 enum FftMode { kC2C = 0, kR2C = 1, kSpec = 2 };
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) {
   return make_float2(a.x + b.x, a.y + b.y);
 }
@@ -242,7 +244,7 @@ struct GlobalIO {
   }
 };
 
-template <int LOG2N, int P, class IO>
+template <int LOG2N, int P, class IO, bool LOWREG = false>
 __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
                                          const Tw<LOG2N, P - 1 < 0 ? 0 : P - 1>& tw) {
   using PL = Plan<LOG2N>;
@@ -268,13 +270,32 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
   for (int b = 0; b < NB; ++b) {
     const int j = j0 + b * PL::TPT;
     const int m = j & (NS - 1);
-    if constexpr (NS > 1) {
+    if constexpr (NS > 1 && !LOWREG) {
       float2 w[R];
       w[1] = tw.w[b];
 #pragma unroll
       for (int r = 2; r < R; ++r) w[r] = (r & 1) ? cmul(w[r - 1], w[1]) : cmul(w[r / 2], w[r / 2]);
 #pragma unroll
       for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[r]);
+    } else if constexpr (NS > 1) {
+      // Few live registers: w1, w2, w4, w8 by squaring, w_r as the product of
+      // the powers in r's binary digits, applied as soon as it is formed.
+      float2 p2[4];
+      p2[0] = tw.w[b];
+#pragma unroll
+      for (int e = 1; e < 4; ++e) p2[e] = cmul(p2[e - 1], p2[e - 1]);
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        float2 w = make_float2(1.f, 0.f);
+        bool first = true;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((r >> e) & 1) {
+            w = first ? p2[e] : cmul(w, p2[e]);
+            first = false;
+          }
+        v[b][r] = cmul(v[b][r], w);
+      }
     }
     dft<R>(v[b]);
     const int base = (j - m) * R + m;
@@ -287,8 +308,8 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
   }
   if constexpr (!LAST) __syncthreads();
   if constexpr (P + 1 < PL::NP) {
-    if constexpr (P == 0) run_pass<LOG2N, P + 1>(io, buf, j0, tw);
-    else run_pass<LOG2N, P + 1>(io, buf, j0, tw.next);
+    if constexpr (P == 0) run_pass<LOG2N, P + 1, IO, LOWREG>(io, buf, j0, tw);
+    else run_pass<LOG2N, P + 1, IO, LOWREG>(io, buf, j0, tw.next);
   }
 }
 
@@ -386,6 +407,189 @@ int launch_spec_real(const FftArgs& a, hipStream_t s) {
   return DSP_OK;
 }
 
+// Transform entirely in LDS (passes after the first, four-step sub-transforms).
+template <int N>
+struct LdsIO {
+  static constexpr bool kLdsIn = true;
+  float2* buf;
+  __device__ __forceinline__ float2 load(int n) const { return buf[lpad(n)]; }
+  __device__ __forceinline__ void store(int k, float2 v) const { buf[lpad(k)] = v; }
+};
+
+// ---------------------------------------------------------------------------
+// Streaming magnitude spectrum (round 3; the default for N = 2^6 .. 2^14 with a
+// first pass of radix < 16): the same real-input transform as k_spec_real,
+// but a persistent grid in which every workgroup walks its transforms in a
+// loop and keeps the next transform's segment in flight while the current one
+// runs its LDS passes, with 16-byte loads:
+//   * pass 0 is remapped so that thread j0 owns the NB0 consecutive
+//     butterflies NB0*j0 .. NB0*j0+NB0-1 (pass 0 has no twiddles, so any
+//     butterfly-to-thread map works): for every r its inputs are NB0
+//     consecutive complex values = 2*NB0 consecutive real samples, i.e. NB0/2
+//     float4 loads per lane, contiguous across the wave;
+//   * the window (the same for every transform) is re-read from L1/L2;
+//   * the prefetched float4s of transform t+G are issued right after the
+//     window multiply of transform t, so HBM latency hides under t's LDS
+//     passes and split (the round-2 kernel issued each transform's loads only
+//     when its workgroup started: SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.71).
+// Rows whose segment start is not 16-byte aligned, or frames past the
+// segment's end, take per-sample guarded loads (same values).
+// ---------------------------------------------------------------------------
+template <int LOG2N>
+struct SpecStream {
+  using PL = Plan<LOG2N - 1>;                 // the N/2-point complex transform
+  static constexpr int N = 1 << LOG2N, NH = N / 2;
+  static constexpr int R0 = PL::radix(0);
+  static constexpr int NB0 = PL::RMAX / R0;    // pass-0 butterflies per thread
+  static constexpr int S0 = NH / R0;           // pass-0 input stride (complex)
+  static constexpr int NQ = NB0 / 2;           // float4s per r
+  static_assert(NB0 >= 2 && NB0 % 2 == 0, "pass 0 needs >= 2 butterflies per thread");
+};
+
+// The transform's pass-0 samples as float4s through a raw buffer resource
+// over its frame: one VGPR offset for all loads (the r strides go to the
+// SGPR/immediate offsets), and bytes past the frame's valid samples -- or the
+// whole frame of a dead transform -- read as zeros (the hardware checks every
+// dword against num_records), which is the zero padding of dsp_core.py:81-82.
+template <int LOG2N>
+__device__ __forceinline__ void spec_stream_load(const FftArgs& a, const InRow& ir, bool live,
+                                                 int j0, f32x4_t (&raw)[SpecStream<LOG2N>::NQ]
+                                                                         [SpecStream<LOG2N>::R0]) {
+  using SS = SpecStream<LOG2N>;
+  const int64_t valid = live ? (ir.valid < SS::N ? (ir.valid > 0 ? ir.valid : 0) : SS::N) : 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.in) + (live ? ir.base : 0), 0, (int)(valid * 4), 0x00020000);
+  const int vo = 4 * 2 * SS::NB0 * j0;  // bytes
+#pragma unroll
+  for (int r = 0; r < SS::R0; ++r)
+#pragma unroll
+    for (int q = 0; q < SS::NQ; ++q)
+      raw[q][r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 4 * 2 * (2 * q + r * SS::S0), 2);
+}
+
+#ifndef DSP_SPEC_WAVES
+#define DSP_SPEC_WAVES 3
+#endif
+template <int LOG2N, int TPBX>
+__global__ __launch_bounds__(TPBX * Plan<LOG2N - 1>::TPT)
+__attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs a, int64_t units) {
+  using SS = SpecStream<LOG2N>;
+  using PL = typename SS::PL;
+  constexpr int NH = SS::NH, R0 = SS::R0, NB0 = SS::NB0, NQ = SS::NQ;
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int tl = threadIdx.x / PL::TPT;
+  const int j0 = threadIdx.x - tl * PL::TPT;
+  float2* buf = lds + tl * PL::PADN;
+  f32x4_t raw[NQ][R0];
+  int64_t u = blockIdx.x;
+  {
+    const int64_t t = u * TPBX + tl;
+    const bool live = u < units && t < a.B;
+    spec_stream_load<LOG2N>(a, in_row<kSpec>(a, live ? t : 0), live, j0, raw);
+  }
+  for (; u < units; u += gridDim.x) {
+    // An opaque copy of the thread's index per iteration: every LDS / table
+    // address below depends only on it, and hoisting them out of the loop
+    // costs ~120 VGPRs (206 vs 84 without the loop).
+    int jj = j0;
+    asm volatile("" : "+v"(jj));
+    const int64_t t = u * TPBX + tl;
+    const bool live = t < a.B;
+    // window the transform's samples (packed even/odd as complex; the window
+    // is re-read from L1/L2 here rather than held in 32 VGPRs across the
+    // passes) ...
+    // (opaque per-iteration table pointers: otherwise the loop-invariant
+    // window and twiddle loads -- and the twiddle powers computed from them --
+    // are hoisted out of the loop into ~100 VGPRs; they are L1 hits)
+    const float* winp = a.win;
+    const float2* twp = a.tw;
+    asm volatile("" : "+s"(winp), "+s"(twp));
+    Tw<LOG2N - 1, 0> tw;
+    load_tw<LOG2N - 1, 0>(tw, twp, jj, 2);
+    float2 v[NB0][R0];
+#pragma unroll
+    for (int r = 0; r < R0; ++r)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const f32x4_t w =
+            *reinterpret_cast<const f32x4_t*>(winp + 2 * (NB0 * jj + 2 * q + r * SS::S0));
+        const f32x4_t x = raw[q][r];
+        v[2 * q][r] = make_float2(x.x * w.x, x.y * w.y);
+        v[2 * q + 1][r] = make_float2(x.z * w.z, x.w * w.w);
+      }
+    // ... and put the next one in flight
+    {
+      const int64_t un = u + gridDim.x;
+      const int64_t tn = un * TPBX + tl;
+      const bool ln = un < units && tn < a.B;
+      spec_stream_load<LOG2N>(a, in_row<kSpec>(a, ln ? tn : 0), ln, jj, raw);
+    }
+    // pass 0 (radix R0, no twiddles) into LDS in Stockham order
+#pragma unroll
+    for (int b = 0; b < NB0; ++b) {
+      dft<R0>(v[b]);
+      const int jb = NB0 * jj + b;
+#pragma unroll
+      for (int r = 0; r < R0; ++r) buf[lpad(jb * R0 + r)] = v[b][r];
+    }
+    __syncthreads();
+    if constexpr (PL::NP > 1)
+      run_pass<LOG2N - 1, 1, LdsIO<NH>, true>(LdsIO<NH>{buf}, buf, jj, tw);
+    __syncthreads();  // the last pass stored Z into LDS
+    if (live) {
+      float* mr = a.out + t * a.ld_out;
+      for (int k = jj; k <= NH / 2; k += PL::TPT) {
+        const float2 zk = buf[lpad(k)];
+        const float2 zm = buf[lpad((NH - k) & (NH - 1))];
+        const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+        const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+        const float2 w = twp[k < NH ? k : 0];
+        const float2 wo = cmul(o, w);
+        const float2 xk = cadd(e, wo), xm = csub(e, wo);
+        mr[k] = sqrtf(fmaf(xk.x, xk.x, xk.y * xk.y));
+        if (k > 0 && k < NH / 2) mr[NH - k] = sqrtf(fmaf(xm.x, xm.x, xm.y * xm.y));
+        if (k == 0) mr[NH] = fabsf(zk.x - zk.y);
+      }
+    }
+    __syncthreads();  // the split's LDS reads precede the next transform's pass 0
+  }
+}
+
+// Resident workgroups per CU for a kernel (asked once per calling thread and
+// kernel instance; thread_local: no state shared between threads).
+template <class Kern>
+int resident_groups(Kern k, int threads, size_t shm) {
+  thread_local int dev = -1, cached = 0;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  if (d != dev || cached <= 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k),
+                                                     threads, shm) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      return 0;
+    dev = d;
+    cached = per_cu * cus;
+  }
+  return cached;
+}
+
+template <int LOG2N>
+int launch_spec_stream(const FftArgs& a, hipStream_t s) {
+  using PL = Plan<LOG2N - 1>;
+  constexpr int TPBX = 1;
+  const size_t shm = (size_t)TPBX * PL::PADN * sizeof(float2);
+  if (int rc = allow_lds(k_spec_stream<LOG2N, TPBX>, shm)) return rc;
+  const int64_t units = ceil_div(a.B, TPBX);
+  const int res = resident_groups(k_spec_stream<LOG2N, TPBX>, TPBX * PL::TPT, shm);
+  DSP_REQUIRE(res > 0, "occupancy query failed");
+  const unsigned grid = (unsigned)(units < res ? units : res);
+  hipLaunchKernelGGL((k_spec_stream<LOG2N, TPBX>), dim3(grid), dim3(TPBX * PL::TPT), shm, s, a,
+                     units);
+  DSP_LAUNCHED("k_spec_stream");
+  return DSP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Four-step FFT for N = 2^15 .. 2^DSP_MAX_LOG2N_FFT (beyond one workgroup's
 // LDS): N = NA * NB, n = n1 + NB n2, k = k2 + NA k1 (n1, k1 < NB; n2, k2 < NA)
@@ -401,14 +605,6 @@ int launch_spec_real(const FftArgs& a, hipStream_t s) {
 // negation).  The workspace holds Y: B x N complex.
 // ---------------------------------------------------------------------------
 constexpr int kCols = 8;
-
-template <int N>
-struct LdsIO {
-  static constexpr bool kLdsIn = true;
-  float2* buf;
-  __device__ __forceinline__ float2 load(int n) const { return buf[lpad(n)]; }
-  __device__ __forceinline__ void store(int k, float2 v) const { buf[lpad(k)] = v; }
-};
 
 __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
   m &= N - 1;
@@ -520,6 +716,18 @@ template <int MODE>
 int dispatch(const FftArgs& a, int log2n, hipStream_t s);
 
 int dispatch_spec(const FftArgs& a, int log2n, hipStream_t s) {
+#if !DSP_SPEC_V1
+  switch (log2n) {  // sizes whose first pass has radix < 16: the streaming kernel
+    case 6: return launch_spec_stream<6>(a, s);
+    case 7: return launch_spec_stream<7>(a, s);
+    case 8: return launch_spec_stream<8>(a, s);
+    case 10: return launch_spec_stream<10>(a, s);
+    case 11: return launch_spec_stream<11>(a, s);
+    case 12: return launch_spec_stream<12>(a, s);
+    case 14: return launch_spec_stream<14>(a, s);
+    default: break;
+  }
+#endif
   switch (log2n) {
     case 5: return launch_spec_real<5>(a, s);
     case 6: return launch_spec_real<6>(a, s);
