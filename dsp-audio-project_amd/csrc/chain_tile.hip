@@ -329,6 +329,26 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
   fence();
 }
 
+// A/B variant (-DDSP_DIRECT_STORE=1): each lane stores its own TS outputs as
+// float4s straight from registers (no LDS staging; a wave-instruction then
+// writes 16 B per lane at a TS*4-byte lane stride, and the lines fill over
+// TS/4 instructions).
+template <int TS>
+__device__ __forceinline__ void store_direct(const float (&v)[TS], int lane,
+                                             __amdgpu_buffer_rsrc_t rs, int64_t m0) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int64_t base = (m0 + (int64_t)lane * TS) * 4;
+#pragma unroll
+  for (int k = 0; k < TS / 4; ++k) {
+    u32x4 d;
+    d.x = __float_as_uint(v[4 * k]);
+    d.y = __float_as_uint(v[4 * k + 1]);
+    d.z = __float_as_uint(v[4 * k + 2]);
+    d.w = __float_as_uint(v[4 * k + 3]);
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)base, 16 * k, kStream);
+  }
+}
+
 // LDS floats store_tile<TS> stages through.
 __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * (ts + 4); }
 
@@ -477,7 +497,11 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   if (a.y) {
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
         a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+#if DSP_DIRECT_STORE
+    store_direct<TS>(y, lane, ry, m0);
+#else
     store_tile<TS>(lds, y, lane, ry, m0);
+#endif
   }
   pin(y);
   // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
@@ -522,7 +546,11 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   int lane_z = lane;
   asm volatile("" : "+v"(lane_z));  // recompute the store offsets (no spill across pass 2)
+#if DSP_DIRECT_STORE
+  store_direct<TS>(y, lane_z, rz, m0);
+#else
   store_tile<TS>(lds, y, lane_z, rz, m0);
+#endif
 }
 
 template <class GEO>

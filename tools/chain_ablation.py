@@ -5,7 +5,8 @@ objects of the in-tree build.  Time them with tools/gpu_libs.sh.
 
     python tools/chain_ablation.py [NAME ...]   (default: all)
 
-NOSRC   y = window samples (no SRC FMAs)     NOP1  no pass-1 sums
+NOSRC   y = window samples (no SRC FMAs)     NOP1  no pass-1 sums (the float32
+        input-normal sums; the float64 change of basis stays)
 NOSCAN  no carry scan                        NOP2  no pass-2 cascade
 NOYST   no y store                           NOZST no z store (also lets the
         compiler drop most of pass 2: read it together with NOP2)
@@ -36,20 +37,21 @@ def patched() -> str:
     parts = "".join(f"    src_part<GEO, {h}, 12>(xw, mt, y);\n    pin(y);\n" for h in (0, 12, 24, 36))
     rep(parts, "#ifdef V_NOSRC\n#pragma unroll\n    for (int i = 0; i < TS; ++i) y[i] = xw[i];\n"
         "    pin(y);\n#else\n" + parts + "#endif\n")
-    rep("#pragma unroll\n  for (int i = 0; i < TS; ++i) {\n    const double u = (double)y[i];",
-        "#ifdef V_NOP1\n#pragma unroll\n  for (int d = 0; d < kD; ++d) v[d] = (double)y[d];\n"
-        "  if (false)\n#endif\n#pragma unroll\n  for (int i = 0; i < TS; ++i) {\n"
-        "    const double u = (double)y[i];")
+    # pass 1 (float32 sums in input-normal coordinates, round 3): keep the
+    # change of basis, drop the 6 v_pk_fma_f32 per sample
+    rep("#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {",
+        "#ifdef V_NOP1\n#pragma unroll\n    for (int d = 0; d < kD; ++d) e2[d] = f32x2{y[d], y[d + 1]};\n"
+        "    if (false)\n#endif\n#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {")
     rep("#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {",
         "#ifndef V_NOSCAN\n#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {")
     rep("  // Entry state of the lane's sub-chunk", "#endif\n  // Entry state of the lane's sub-chunk")
-    rep("  store_tile<GEO>(lds, y, lane, ry, m0);\n",
-        "#ifndef V_NOYST\n  store_tile<GEO>(lds, y, lane, ry, m0);\n#endif\n")
+    rep("    store_tile<TS>(lds, y, lane, ry, m0);\n",
+        "#ifndef V_NOYST\n    store_tile<TS>(lds, y, lane, ry, m0);\n#endif\n")
     rep("  {\n    double pend[kS];",
         "#ifdef V_NOP2\n  for (int t = 0; t < TS; ++t) y[t] = clip_f32(y[t] + (float)s1[t % kS], lo, hi);\n"
         "  if (false)\n#endif\n  {\n    double pend[kS];")
-    rep("  store_tile<GEO>(lds, y, lane_z, rz, m0);",
-        "#ifndef V_NOZST\n  store_tile<GEO>(lds, y, lane_z, rz, m0);\n#else\n"
+    rep("  store_tile<TS>(lds, y, lane_z, rz, m0);",
+        "#ifndef V_NOZST\n  store_tile<TS>(lds, y, lane_z, rz, m0);\n#else\n"
         "  if (y[0] == 12345.f) a.z[0] = y[1];\n#endif")
     return s
 
