@@ -596,15 +596,22 @@ int launch_spec_stream(const FftArgs& a, hipStream_t s) {
 //   step A: Y[n1][k2] = W_N^(n1 k2) * sum_n2 x[n1 + NB n2] W_NA^(n2 k2)
 //           -> workspace[k2][n1]
 //   step B: X[k2 + NA k1] = sum_n1 Y[n1][k2] W_NB^(n1 k1)
-// Each workgroup runs kCols sub-transforms of consecutive columns (step A) or
+// Each workgroup runs KC sub-transforms of consecutive columns (step A) or
 // rows (step B) in LDS with the one-launch Stockham passes; the HBM side of
-// both steps moves kCols consecutive complex values (64 B) per index, staged
-// through LDS so every global access is a run of consecutive addresses.  The
+// both steps moves KC consecutive complex values per index (8 -- 64 B -- for
+// sub-transforms up to 2^11; 4, 2, 1 for 2^12, 2^13, 2^14, whose LDS images
+// are larger: round 3 took the limit from 2^22 to 2^26), staged through LDS so
+// every global access is a run of consecutive addresses.  The
 // sub-transforms' twiddles come from the caller's W_N table at stride N/NA
 // (N/NB), the inter-step twiddle W_N^m from the same table (m < N/2, else its
 // negation).  The workspace holds Y: B x N complex.
 // ---------------------------------------------------------------------------
 constexpr int kCols = 8;
+// Columns per workgroup for a sub-transform of 2^LOG2 points: KC images of
+// (N + N/16 + 1) complex values within 160 KB of LDS.
+__host__ __device__ constexpr int kcols_for(int log2) {
+  return log2 <= 11 ? kCols : log2 == 12 ? 4 : log2 == 13 ? 2 : 1;
+}
 
 __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
   m &= N - 1;
@@ -619,17 +626,18 @@ struct Fft4Args {
 };
 
 template <int LOG2A, int MODE>
-__global__ __launch_bounds__(kCols * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
+__global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
   using PL = Plan<LOG2A>;
-  constexpr int NA = PL::N, NT = kCols * PL::TPT, TS = PL::PADN + 1;
+  constexpr int KC = kcols_for(LOG2A);
+  constexpr int NA = PL::N, NT = KC * PL::TPT, TS = PL::PADN + 1;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const FftArgs& a = f.a;
   const int64_t NB = f.N / NA;
   const int64_t b = blockIdx.y;
-  const int64_t c0 = (int64_t)blockIdx.x * kCols;
+  const int64_t c0 = (int64_t)blockIdx.x * KC;
   const InRow ir = in_row<MODE>(a, b);
-  for (int i = threadIdx.x; i < kCols * NA; i += NT) {
-    const int c = i % kCols, n2 = i / kCols;
+  for (int i = threadIdx.x; i < KC * NA; i += NT) {
+    const int c = i % KC, n2 = i / KC;
     lds[c * TS + lpad(n2)] = load_input<MODE>(a, ir, (int)(c0 + c + NB * n2), true);
   }
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
@@ -639,24 +647,25 @@ __global__ __launch_bounds__(kCols * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f)
   run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
   __syncthreads();
   float2* y = f.ws + b * f.N;
-  for (int i = threadIdx.x; i < kCols * NA; i += NT) {
-    const int c = i % kCols, k2 = i / kCols;
+  for (int i = threadIdx.x; i < KC * NA; i += NT) {
+    const int c = i % KC, k2 = i / KC;
     const int64_t n1 = c0 + c;
     y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], tw_full(a.tw, n1 * k2, f.N));
   }
 }
 
 template <int LOG2B, int MODE>
-__global__ __launch_bounds__(kCols * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
+__global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
   using PL = Plan<LOG2B>;
-  constexpr int NB = PL::N, NT = kCols * PL::TPT, TS = PL::PADN + 1;
+  constexpr int KC = kcols_for(LOG2B);
+  constexpr int NB = PL::N, NT = KC * PL::TPT, TS = PL::PADN + 1;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const FftArgs& a = f.a;
   const int64_t NA = f.N / NB;
   const int64_t b = blockIdx.y;
-  const int64_t r0 = (int64_t)blockIdx.x * kCols;  // first k2 row
+  const int64_t r0 = (int64_t)blockIdx.x * KC;  // first k2 row
   const float2* y = f.ws + b * f.N;
-  for (int i = threadIdx.x; i < kCols * NB; i += NT) {
+  for (int i = threadIdx.x; i < KC * NB; i += NT) {
     const int r = i / NB, n1 = i - r * NB;
     lds[r * TS + lpad(n1)] = y[(r0 + r) * NB + n1];
   }
@@ -666,8 +675,8 @@ __global__ __launch_bounds__(kCols * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f)
   __syncthreads();
   run_pass<LOG2B, 0>(LdsIO<NB>{lds + tl * TS}, lds + tl * TS, j0, tw);
   __syncthreads();
-  for (int i = threadIdx.x; i < kCols * NB; i += NT) {
-    const int c = i % kCols, k1 = i / kCols;
+  for (int i = threadIdx.x; i < KC * NB; i += NT) {
+    const int c = i % KC, k1 = i / KC;
     const int64_t k = r0 + c + NA * k1;
     const float2 v = lds[c * TS + lpad(k1)];
     if constexpr (MODE == kSpec) {
@@ -683,16 +692,17 @@ int launch_fft4(const Fft4Args& f, hipStream_t s) {
   using PA = Plan<LOG2A>;
   using PB = Plan<LOG2B>;
   static_assert(LOG2A >= 4 && LOG2B >= LOG2A, "split");
-  const size_t sa = (size_t)kCols * (PA::PADN + 1) * sizeof(float2);
-  const size_t sb = (size_t)kCols * (PB::PADN + 1) * sizeof(float2);
+  constexpr int KA = kcols_for(LOG2A), KB = kcols_for(LOG2B);
+  const size_t sa = (size_t)KA * (PA::PADN + 1) * sizeof(float2);
+  const size_t sb = (size_t)KB * (PB::PADN + 1) * sizeof(float2);
   if (int rc = allow_lds(k_fft4_a<LOG2A, MODE>, sa)) return rc;
   if (int rc = allow_lds(k_fft4_b<LOG2B, MODE>, sb)) return rc;
   const unsigned rows = (unsigned)f.a.B;
-  hipLaunchKernelGGL((k_fft4_a<LOG2A, MODE>), dim3((unsigned)(PB::N / kCols), rows),
-                     dim3(kCols * PA::TPT), sa, s, f);
+  hipLaunchKernelGGL((k_fft4_a<LOG2A, MODE>), dim3((unsigned)(PB::N / KA), rows),
+                     dim3(KA * PA::TPT), sa, s, f);
   DSP_LAUNCHED("k_fft4_a");
-  hipLaunchKernelGGL((k_fft4_b<LOG2B, MODE>), dim3((unsigned)(PA::N / kCols), rows),
-                     dim3(kCols * PB::TPT), sb, s, f);
+  hipLaunchKernelGGL((k_fft4_b<LOG2B, MODE>), dim3((unsigned)(PA::N / KB), rows),
+                     dim3(KB * PB::TPT), sb, s, f);
   DSP_LAUNCHED("k_fft4_b");
   return DSP_OK;
 }
@@ -708,6 +718,10 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
     case 20: return launch_fft4<10, 10, MODE>(f, s);
     case 21: return launch_fft4<10, 11, MODE>(f, s);
     case 22: return launch_fft4<11, 11, MODE>(f, s);
+    case 23: return launch_fft4<11, 12, MODE>(f, s);
+    case 24: return launch_fft4<12, 12, MODE>(f, s);
+    case 25: return launch_fft4<12, 13, MODE>(f, s);
+    case 26: return launch_fft4<13, 13, MODE>(f, s);
     default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
   }
 }

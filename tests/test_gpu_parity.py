@@ -673,7 +673,8 @@ def test_shards_plan_with_the_job_batch(gpu):
 def test_fft_four_step_matches_reference(gpu):
     """N = 2^13 .. 2^16 through the drop-in against the reference's own outputs
     (tests/golden/fft_large.npz; 2^15 and 2^16 take the four-step path), and
-    2^17 .. 2^22 batched against np.fft.fft: max|dX| <= 1e-5 * max|X|."""
+    2^17 .. 2^22 batched and 2^23 / 2^24 / 2^26 against np.fft.fft:
+    max|dX| <= 1e-5 * max|X|; 2^27 raises RuntimeError."""
     dc = _dc()
     g = golden("fft_large")
     for k in (13, 14, 15, 16):
@@ -696,8 +697,20 @@ def test_fft_four_step_matches_reference(gpu):
     X = _ops().fft(torch.from_numpy(xr).to(gpu)).cpu().numpy()
     ref = np.fft.fft(xr.astype(np.float64), axis=1)
     assert np.max(np.abs(X - ref)) <= FFT_RTOL * np.max(np.abs(ref))
+    # 2^23 .. 2^26 (round 3): sub-transforms of 2^12 / 2^13 points with 4 / 2
+    # columns per workgroup; one row each, real and complex input
+    for lg, real in ((23, True), (24, False), (26, True)):
+        n = 1 << lg
+        x = rng.uniform(-1, 1, n).astype(np.float32)
+        if not real:
+            x = (x + 1j * rng.uniform(-1, 1, n).astype(np.float32)).astype(np.complex64)
+        X = _ops().fft(torch.from_numpy(x[None, :]).to(gpu)).cpu().numpy()[0]
+        ref = np.fft.fft(x.astype(np.complex128))
+        err = np.max(np.abs(X - ref))
+        assert err <= FFT_RTOL * np.max(np.abs(ref)), (lg, err)
+        del X, ref
     with pytest.raises(RuntimeError):
-        _ops().fft(torch.zeros((1, 1 << 23), device=gpu))
+        _ops().fft(torch.zeros((1, 1 << 27), device=gpu))
 
 
 def test_spectrum_four_step_matches_reference(gpu):
