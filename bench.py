@@ -457,7 +457,16 @@ def main(argv=None):
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("gloo")      # timing barrier + max only: no RCCL
+        # gloo prints its connection banner on stdout from C++; keep stdout for
+        # the one JSON line (the banner goes to stderr).
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            tdist.init_process_group("gloo")  # timing barrier + max only: no RCCL
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         dist = tdist
     if dry:
         r = measure_stub(wl, B, args.steps)

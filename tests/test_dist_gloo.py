@@ -92,8 +92,8 @@ def test_bench_gpus_flag_launches_the_ranks_itself():
                           "--steps", "3", "--warmup", "1"], capture_output=True, text=True,
                          timeout=300, env=_bench_env(), cwd=root)
     assert res.returncode == 0, res.stderr[-2000:]
-    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, res.stdout
+    lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), res.stdout   # stdout: the JSON line only
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3
     assert out["config"]["total_channels"] == 32768
