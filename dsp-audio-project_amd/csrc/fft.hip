@@ -468,7 +468,13 @@ __device__ __forceinline__ void spec_stream_load(const FftArgs& a, const InRow& 
 }
 
 #ifndef DSP_SPEC_WAVES
-#define DSP_SPEC_WAVES 3
+#define DSP_SPEC_WAVES 3   // waves per SIMD the streaming kernel is compiled for
+#endif
+#ifndef DSP_SPEC_TPBX
+#define DSP_SPEC_TPBX 2    // transforms per workgroup (1: same at 32768 ch, 8 % slower at 4096)
+#endif
+#ifndef DSP_SPEC_LOWREG
+#define DSP_SPEC_LOWREG 1  // twiddle powers by squaring (few live VGPRs)
 #endif
 template <int LOG2N, int TPBX>
 __global__ __launch_bounds__(TPBX * Plan<LOG2N - 1>::TPT)
@@ -534,7 +540,7 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
     }
     __syncthreads();
     if constexpr (PL::NP > 1)
-      run_pass<LOG2N - 1, 1, LdsIO<NH>, true>(LdsIO<NH>{buf}, buf, jj, tw);
+      run_pass<LOG2N - 1, 1, LdsIO<NH>, DSP_SPEC_LOWREG>(LdsIO<NH>{buf}, buf, jj, tw);
     __syncthreads();  // the last pass stored Z into LDS
     if (live) {
       float* mr = a.out + t * a.ld_out;
@@ -577,7 +583,7 @@ int resident_groups(Kern k, int threads, size_t shm) {
 template <int LOG2N>
 int launch_spec_stream(const FftArgs& a, hipStream_t s) {
   using PL = Plan<LOG2N - 1>;
-  constexpr int TPBX = 1;
+  constexpr int TPBX = DSP_SPEC_TPBX;
   const size_t shm = (size_t)TPBX * PL::PADN * sizeof(float2);
   if (int rc = allow_lds(k_spec_stream<LOG2N, TPBX>, shm)) return rc;
   const int64_t units = ceil_div(a.B, TPBX);

@@ -15,7 +15,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 tail -1 "$OUT/smoke.log"
 for c in c4 c5; do
   echo "== bench $c"
-  timeout -k 10 600 python bench.py --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
+  extra=""; [ $c = c5 ] && extra="--no-extras"
+  timeout -k 10 600 python bench.py --config $c $extra > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -20 "$OUT/bench_$c.err"; exit 1; }
   cut -c1-300 "$OUT/bench_$c.json"
 done
 cd /tmp && export TMPDIR=/tmp
@@ -29,5 +30,6 @@ done
 cd "$GRAFT_REPO_ROOT"
 bash tools/pmc_chain.sh "$TAG/pmc_c4" 3 c4 > "$OUT/pmc_c4.log" 2>&1 || { tail -20 "$OUT/pmc_c4.log"; exit 1; }
 bash tools/pmc_chain.sh "$TAG/pmc_c5" 3 c5 > "$OUT/pmc_c5.log" 2>&1 || { tail -20 "$OUT/pmc_c5.log"; exit 1; }
-grep -E "^==|traffic" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c4/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c5/pmc_summary.txt"
+bash tools/pmc_chain.sh "$TAG/pmc_c3" 3 c3 > "$OUT/pmc_c3.log" 2>&1 || { tail -20 "$OUT/pmc_c3.log"; exit 1; }
+grep -E "^==|traffic" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c4/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c5/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c3/pmc_summary.txt"
 echo done
