@@ -260,6 +260,11 @@ int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info) {
   return dsp::wav_parse(file, len, info);
 }
 
+int dsp_audio_parse(const uint8_t* file, size_t len, dsp_wav_info* info) {
+  dsp::clear_error();
+  return dsp::audio_parse(file, len, info);
+}
+
 int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t channels,
                         int64_t B, int64_t frames, int64_t ld_bytes, float* out,
                         int64_t ld_out, void* stream) {

@@ -29,61 +29,94 @@ namespace {
 
 constexpr int kIoNT = 256;
 
-// Sample c of frame i as soundfile returns it (float64).
-template <int FMT, int BITS>
+// Byte k of a W-byte little-endian value stored little- or big-endian.
+template <int W, bool BE>
+__device__ __forceinline__ uint32_t byte_at(const uint8_t* __restrict__ p, int k) {
+  return p[BE ? W - 1 - k : k];
+}
+
+// G.711 expansions to 16-bit linear PCM, as libsndfile's tables (and the
+// classic Sun g711.c) give them: mu-law peaks at +-32124, A-law at +-32256.
+__device__ __forceinline__ int ulaw_to_s16(uint32_t u) {
+  u = ~u & 0xFFu;
+  const int t = ((((int)(u & 0x0F)) << 3) + 0x84) << ((u >> 4) & 7);
+  return (u & 0x80) ? (0x84 - t) : (t - 0x84);
+}
+__device__ __forceinline__ int alaw_to_s16(uint32_t a) {
+  a ^= 0x55;
+  int t = (int)(a & 0x0F) << 4;
+  const int seg = (int)((a & 0x70) >> 4);
+  if (seg == 0) t += 8;
+  else t = (t + 0x108) << (seg - 1);
+  return (a & 0x80) ? t : -t;
+}
+
+// Sample c of frame i as soundfile returns it (float64).  FMT: DSP_WAV_PCM /
+// FLOAT / ALAW / ULAW; BE: big-endian samples (AIFF); S8: signed 8-bit PCM
+// (AIFF; WAV's is unsigned with a 128 offset).
+template <int FMT, int BITS, bool BE = false, bool S8 = false>
 __device__ __forceinline__ double decode(const uint8_t* __restrict__ p) {
-  if constexpr (FMT == DSP_WAV_FLOAT) {
+  constexpr int W = BITS / 8;
+  if constexpr (FMT == DSP_WAV_ULAW) {
+    return (double)ulaw_to_s16(p[0]) / 32768.0;
+  } else if constexpr (FMT == DSP_WAV_ALAW) {
+    return (double)alaw_to_s16(p[0]) / 32768.0;
+  } else if constexpr (FMT == DSP_WAV_FLOAT) {
     if constexpr (BITS == 32) {
-      float f;
-      memcpy(&f, p, 4);
-      return (double)f;
+      uint32_t u = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u |= byte_at<4, BE>(p, k) << (8 * k);
+      return (double)__uint_as_float(u);
     } else {
-      double d;
-      memcpy(&d, p, 8);
-      return d;
+      uint64_t u = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u |= (uint64_t)byte_at<8, BE>(p, k) << (8 * k);
+      return __longlong_as_double((long long)u);
     }
   } else if constexpr (BITS == 8) {
-    return ((double)p[0] - 128.0) / 128.0;
+    return S8 ? (double)(int8_t)p[0] / 128.0 : ((double)p[0] - 128.0) / 128.0;
   } else if constexpr (BITS == 16) {
-    const int16_t v = (int16_t)(p[0] | (p[1] << 8));
+    const int16_t v = (int16_t)(byte_at<2, BE>(p, 0) | (byte_at<2, BE>(p, 1) << 8));
     return (double)v / 32768.0;
   } else if constexpr (BITS == 24) {
-    int32_t v = p[0] | (p[1] << 8) | (p[2] << 16);
-    v = (v << 8) >> 8;  // sign-extend
+    int32_t v = (int32_t)(byte_at<3, BE>(p, 0) | (byte_at<3, BE>(p, 1) << 8) |
+                          (byte_at<3, BE>(p, 2) << 16));
+    v = (int32_t)((uint32_t)v << 8) >> 8;  // sign-extend
     return (double)v / 8388608.0;
   } else {
-    const int32_t v = (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) |
-                                ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+    static_assert(W == 4, "PCM widths 8/16/24/32");
+    const int32_t v = (int32_t)(byte_at<4, BE>(p, 0) | (byte_at<4, BE>(p, 1) << 8) |
+                                (byte_at<4, BE>(p, 2) << 16) | (byte_at<4, BE>(p, 3) << 24));
     return (double)v / 2147483648.0;
   }
 }
 
 // np.add.reduce over a contiguous axis of length ch, then / ch: a plain loop
 // below 8 elements, numpy's 8-accumulator pairwise block up to 128.
-template <int FMT, int BITS>
+template <int FMT, int BITS, bool BE, bool S8>
 __device__ __forceinline__ double channel_mean(const uint8_t* __restrict__ f, int ch) {
   constexpr int W = BITS / 8;
-  if (ch == 1) return decode<FMT, BITS>(f);
+  if (ch == 1) return decode<FMT, BITS, BE, S8>(f);
   double s;
   if (ch < 8) {
-    s = decode<FMT, BITS>(f);
-    for (int c = 1; c < ch; ++c) s += decode<FMT, BITS>(f + c * W);
+    s = decode<FMT, BITS, BE, S8>(f);
+    for (int c = 1; c < ch; ++c) s += decode<FMT, BITS, BE, S8>(f + c * W);
   } else {
     double r[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = decode<FMT, BITS>(f + k * W);
+    for (int k = 0; k < 8; ++k) r[k] = decode<FMT, BITS, BE, S8>(f + k * W);
     int c = 8;
     for (; c + 8 <= ch; c += 8) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] += decode<FMT, BITS>(f + (c + k) * W);
+      for (int k = 0; k < 8; ++k) r[k] += decode<FMT, BITS, BE, S8>(f + (c + k) * W);
     }
     s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; c < ch; ++c) s += decode<FMT, BITS>(f + c * W);
+    for (; c < ch; ++c) s += decode<FMT, BITS, BE, S8>(f + c * W);
   }
   return s / (double)ch;
 }
 
-template <int FMT, int BITS>
+template <int FMT, int BITS, bool BE, bool S8>
 __global__ __launch_bounds__(kIoNT) void k_pcm_mono(const uint8_t* __restrict__ pcm, int ch,
                                                    int64_t frames, int64_t ld_bytes,
                                                    float* __restrict__ out, int64_t ld_out) {
@@ -92,7 +125,7 @@ __global__ __launch_bounds__(kIoNT) void k_pcm_mono(const uint8_t* __restrict__ 
   float* o = out + b * ld_out;
   const int64_t stride = (int64_t)gridDim.x * kIoNT;
   for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < frames; i += stride)
-    o[i] = (float)channel_mean<FMT, BITS>(row + i * (int64_t)ch * (BITS / 8), ch);
+    o[i] = (float)channel_mean<FMT, BITS, BE, S8>(row + i * (int64_t)ch * (BITS / 8), ch);
 }
 
 // Row max of |x| as float bits (all non-negative, so unsigned order is float
@@ -233,12 +266,118 @@ int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
   } else if (tag == 3) {
     w.format = DSP_WAV_FLOAT;
     DSP_REQUIRE(w.bits == 32 || w.bits == 64, "unsupported float width %d", w.bits);
+  } else if (tag == 6 || tag == 7) {  // WAVE_FORMAT_ALAW / WAVE_FORMAT_MULAW (G.711)
+    w.format = tag == 6 ? DSP_WAV_ALAW : DSP_WAV_ULAW;
+    DSP_REQUIRE(w.bits == 8, "G.711 samples must be 8 bits, not %d", w.bits);
   } else {
     return set_error(DSP_EINVAL, "unsupported WAVE format tag %d", tag);
   }
   w.frames = w.data_bytes / ((int64_t)w.channels * (w.bits / 8));
   *info = w;
   return DSP_OK;
+}
+
+namespace {
+uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+// IEEE 754 80-bit extended (AIFF's COMM sampleRate) -> integer Hz, truncated
+// as libsndfile's tenbytefloat2int does; 0 for anything not a finite rate.
+int32_t ext80_to_int(const uint8_t* p) {
+  const int exp = ((p[0] & 0x7F) << 8) | p[1];
+  uint64_t mant = 0;
+  for (int i = 0; i < 8; ++i) mant = (mant << 8) | p[2 + i];
+  if ((p[0] & 0x80) || exp == 0x7FFF || mant == 0) return 0;
+  const int shift = exp - 16383 - 63;  // value = mant * 2^shift
+  if (shift >= 0 || shift < -63) return 0;  // >= 2^63 Hz or < 1 Hz
+  const uint64_t v = mant >> (-shift);
+  return v > 0x7FFFFFFFull ? 0 : (int32_t)v;
+}
+}  // namespace
+
+// FORM/AIFF and FORM/AIFC (what soundfile reads through libsndfile): COMM gives
+// channels, frames, width and the 80-bit rate; AIFC adds the compression
+// type ('NONE'/'twos' big-endian PCM, 'sowt' little-endian PCM, 'fl32'/'fl64'
+// big-endian IEEE float, 'ulaw'/'alaw' G.711); SSND holds the samples after
+// its offset field.  AIFF 8-bit PCM is signed.
+int aiff_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
+  DSP_REQUIRE(buf && info, "null pointer");
+  DSP_REQUIRE(len >= 12 && !memcmp(buf, "FORM", 4) &&
+                  (!memcmp(buf + 8, "AIFF", 4) || !memcmp(buf + 8, "AIFC", 4)),
+              "not a FORM/AIFF file");
+  const bool aifc = !memcmp(buf + 8, "AIFC", 4);
+  bool have_comm = false;
+  int64_t comm_frames = 0;
+  uint8_t comp[4] = {'N', 'O', 'N', 'E'};
+  dsp_wav_info w{};
+  size_t pos = 12;
+  while (pos + 8 <= len) {
+    const uint32_t sz = be32(buf + pos + 4);
+    const uint8_t* body = buf + pos + 8;
+    const size_t avail = len - (pos + 8);
+    if (!memcmp(buf + pos, "COMM", 4)) {
+      DSP_REQUIRE(sz >= 18 && avail >= 18, "truncated COMM chunk");
+      w.channels = be16(body);
+      comm_frames = be32(body + 2);
+      w.bits = be16(body + 6);
+      w.sample_rate = ext80_to_int(body + 8);
+      if (aifc) {
+        DSP_REQUIRE(sz >= 22 && avail >= 22, "truncated AIFC COMM chunk");
+        memcpy(comp, body + 18, 4);
+      }
+      have_comm = true;
+    } else if (!memcmp(buf + pos, "SSND", 4)) {
+      DSP_REQUIRE(have_comm, "SSND chunk before COMM chunk");
+      DSP_REQUIRE(sz >= 8 && avail >= 8, "truncated SSND chunk");
+      const uint32_t off = be32(body);
+      const size_t chunk = sz <= avail ? sz : avail;  // a streamed size may run past the end
+      DSP_REQUIRE((size_t)off + 8 <= chunk, "SSND offset %u past the chunk", off);
+      w.data_offset = (int64_t)(pos + 16 + off);
+      w.data_bytes = (int64_t)(chunk - 8 - off);
+      break;
+    }
+    pos += 8 + (size_t)sz + (sz & 1);
+  }
+  DSP_REQUIRE(have_comm && w.data_offset > 0, "no COMM/SSND chunk");
+  DSP_REQUIRE(w.channels >= 1 && w.channels <= 128, "channels=%d outside [1, 128]", w.channels);
+  DSP_REQUIRE(w.sample_rate > 0, "sample rate not a positive integer");
+  int width = 0;
+  if (!memcmp(comp, "NONE", 4) || !memcmp(comp, "twos", 4) || !memcmp(comp, "sowt", 4)) {
+    DSP_REQUIRE(w.bits == 8 || w.bits == 16 || w.bits == 24 || w.bits == 32,
+                "unsupported PCM width %d", w.bits);
+    const bool le = !memcmp(comp, "sowt", 4);
+    w.format = DSP_WAV_PCM | (le ? 0 : DSP_AUDIO_BE) | (w.bits == 8 ? DSP_AUDIO_S8 : 0);
+    width = w.bits / 8;
+  } else if (!memcmp(comp, "fl32", 4) || !memcmp(comp, "FL32", 4)) {
+    w.format = DSP_WAV_FLOAT | DSP_AUDIO_BE;
+    w.bits = 32;
+    width = 4;
+  } else if (!memcmp(comp, "fl64", 4) || !memcmp(comp, "FL64", 4)) {
+    w.format = DSP_WAV_FLOAT | DSP_AUDIO_BE;
+    w.bits = 64;
+    width = 8;
+  } else if (!memcmp(comp, "ulaw", 4) || !memcmp(comp, "ULAW", 4) ||
+             !memcmp(comp, "alaw", 4) || !memcmp(comp, "ALAW", 4)) {
+    const bool mu = comp[0] == 'u' || comp[0] == 'U';
+    w.format = (mu ? DSP_WAV_ULAW : DSP_WAV_ALAW) | DSP_AUDIO_BE;
+    w.bits = 8;  // COMM says 16 (the decoded width); one byte per sample is stored
+    width = 1;
+  } else {
+    return set_error(DSP_EINVAL, "unsupported AIFF-C compression '%c%c%c%c'", comp[0], comp[1],
+                     comp[2], comp[3]);
+  }
+  const int64_t stored = w.data_bytes / ((int64_t)w.channels * width);
+  w.frames = comm_frames < stored ? comm_frames : stored;
+  *info = w;
+  return DSP_OK;
+}
+
+int audio_parse(const uint8_t* buf, size_t len, dsp_wav_info* info) {
+  DSP_REQUIRE(buf && info, "null pointer");
+  if (len >= 4 && !memcmp(buf, "FORM", 4)) return aiff_parse(buf, len, info);
+  return wav_parse(buf, len, info);
 }
 
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames) {
@@ -266,29 +405,44 @@ int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames)
 int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t B,
                     int64_t frames, int64_t ld_bytes, float* out, int64_t ld_out, hipStream_t s) {
   DSP_REQUIRE(B >= 0 && frames >= 0 && channels >= 1 && channels <= 128, "bad sizes");
+  DSP_REQUIRE(bits == 8 || bits == 16 || bits == 24 || bits == 32 || bits == 64,
+              "unsupported sample width %d", bits);
   DSP_REQUIRE(ld_bytes >= frames * channels * (bits / 8) && ld_out >= frames,
               "leading dimension too small");
   if (B == 0 || frames == 0) return DSP_OK;
   DSP_REQUIRE(pcm && out, "null pointer");
   const uint8_t* p = static_cast<const uint8_t*>(pcm);
-#define DSP_PCM(F, BI)                                                                        \
-  if (format == F && bits == BI) {                                                            \
+#define DSP_PCM(F, BI, FLAGS)                                                                 \
+  if (format == ((F) | (FLAGS)) && bits == BI) {                                              \
     return for_row_ranges(B, [&](int64_t b0, int64_t nb) {                                    \
-      hipLaunchKernelGGL((k_pcm_mono<F, BI>), dim3(io_blocks(frames), (unsigned)nb),          \
-                         dim3(kIoNT), 0, s, p + b0 * ld_bytes, channels, frames, ld_bytes,    \
-                         out + b0 * ld_out, ld_out);                                          \
+      hipLaunchKernelGGL((k_pcm_mono<F, BI, ((FLAGS) & DSP_AUDIO_BE) != 0,                    \
+                                     ((FLAGS) & DSP_AUDIO_S8) != 0>),                         \
+                         dim3(io_blocks(frames), (unsigned)nb), dim3(kIoNT), 0, s,            \
+                         p + b0 * ld_bytes, channels, frames, ld_bytes, out + b0 * ld_out,    \
+                         ld_out);                                                             \
       DSP_LAUNCHED("k_pcm_mono");                                                             \
       return DSP_OK;                                                                          \
     });                                                                                       \
   }
-  DSP_PCM(DSP_WAV_PCM, 8)
-  DSP_PCM(DSP_WAV_PCM, 16)
-  DSP_PCM(DSP_WAV_PCM, 24)
-  DSP_PCM(DSP_WAV_PCM, 32)
-  DSP_PCM(DSP_WAV_FLOAT, 32)
-  DSP_PCM(DSP_WAV_FLOAT, 64)
+  DSP_PCM(DSP_WAV_PCM, 8, 0)                       // WAV: unsigned 8-bit
+  DSP_PCM(DSP_WAV_PCM, 8, DSP_AUDIO_S8)            // AIFF: signed 8-bit
+  DSP_PCM(DSP_WAV_PCM, 8, DSP_AUDIO_S8 | DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_PCM, 16, 0)
+  DSP_PCM(DSP_WAV_PCM, 24, 0)
+  DSP_PCM(DSP_WAV_PCM, 32, 0)
+  DSP_PCM(DSP_WAV_PCM, 16, DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_PCM, 24, DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_PCM, 32, DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_FLOAT, 32, 0)
+  DSP_PCM(DSP_WAV_FLOAT, 64, 0)
+  DSP_PCM(DSP_WAV_FLOAT, 32, DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_FLOAT, 64, DSP_AUDIO_BE)
+  DSP_PCM(DSP_WAV_ULAW, 8, 0)
+  DSP_PCM(DSP_WAV_ALAW, 8, 0)
+  DSP_PCM(DSP_WAV_ULAW, 8, DSP_AUDIO_BE)           // AIFF-C 'ulaw' / 'alaw' (byte order moot)
+  DSP_PCM(DSP_WAV_ALAW, 8, DSP_AUDIO_BE)
 #undef DSP_PCM
-  return set_error(DSP_EINVAL, "unsupported sample format %d / %d bits", format, bits);
+  return set_error(DSP_EINVAL, "unsupported sample format 0x%x / %d bits", format, bits);
 }
 
 int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,

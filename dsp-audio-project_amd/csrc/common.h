@@ -111,6 +111,8 @@ size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 
 // Audio I/O (audio_io.hip).
 int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
+int aiff_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
+int audio_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames);
 int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t B,
                     int64_t frames, int64_t ld_bytes, float* out, int64_t ld_out, hipStream_t s);

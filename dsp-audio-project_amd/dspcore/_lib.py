@@ -76,6 +76,7 @@ _SIGNATURES = {
         _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64),
         ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "dsp_wav_parse": (ctypes.c_int, [ctypes.c_char_p, _c_sz, _vp]),
+    "dsp_audio_parse": (ctypes.c_int, [ctypes.c_char_p, _c_sz, _vp]),
     "dsp_pcm_to_mono_f32": (ctypes.c_int, [
         _vp, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "dsp_peak_normalize_f32": (ctypes.c_int, [
@@ -89,6 +90,10 @@ _SIGNATURES = {
 DSP_TRACE_NAME = 32
 DSP_WAV_PCM = 1
 DSP_WAV_FLOAT = 3
+DSP_WAV_ALAW = 6
+DSP_WAV_ULAW = 7
+DSP_AUDIO_BE = 0x100
+DSP_AUDIO_S8 = 0x200
 
 
 class WavInfo(ctypes.Structure):

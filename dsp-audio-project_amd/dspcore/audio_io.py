@@ -1,13 +1,15 @@
 """Audio I/O edges of the hot path on the GPU.
 
 Loader (reference modules/dsp_core.py:10-35, cargar_senal_audio): the host
-parses the RIFF/WAVE header only (dsp_wav_parse); the raw sample bytes go to
-the device as they are and libdspcore decodes, averages the channels and
-peak-normalises there (dsp_pcm_to_mono_f32, dsp_peak_normalize_f32), with the
-reference's arithmetic (soundfile's float64 scaling, numpy's channel mean,
-float32 cast, float32 division by the peak when it exceeds 1e-6).  Files that
-are not WAV are decoded by soundfile on the host when it is installed (it is
-not in this image) and take the same device path as float64 samples.
+parses the header only (dsp_audio_parse: RIFF/WAVE with PCM, IEEE float and
+G.711 A-law/mu-law, FORM/AIFF and AIFF-C with big- or little-endian PCM,
+'fl32'/'fl64' and G.711); the raw sample bytes go to the device as they are
+and libdspcore decodes, averages the channels and peak-normalises there
+(dsp_pcm_to_mono_f32, dsp_peak_normalize_f32), with the reference's arithmetic
+(soundfile's float64 scaling, numpy's channel mean, float32 cast, float32
+division by the peak when it exceeds 1e-6).  Other containers (FLAC, Ogg, ...)
+are decoded by soundfile on the host when it is installed (it is not in this
+image) and take the same device path as float64 samples.
 
 Playback (reference app.py:349-355): dsp_quantize_pcm16 turns the chain's z
 into 16-bit PCM on the device (nan_to_num, / max|z|, * 32767, truncation) and
@@ -52,12 +54,20 @@ def parse_wav(data: bytes) -> _lib.WavInfo:
     return info
 
 
+def parse_audio(data: bytes) -> _lib.WavInfo:
+    """RIFF/WAVE or FORM/AIFF(-C) header (dsp_audio_parse, host only)."""
+    info = _lib.WavInfo()
+    rc = _lib.load().dsp_audio_parse(data, len(data), ctypes.byref(info))
+    _lib.check(rc, "dsp_audio_parse")
+    return info
+
+
 def _decode_other(data: bytes) -> tuple[np.ndarray, int]:
-    """Non-WAV input: soundfile's host decoder, as the reference (float64)."""
+    """Other containers: soundfile's host decoder, as the reference (float64)."""
     try:
         import soundfile as sf
     except ImportError as e:
-        raise ValueError("not a WAV file and soundfile is not installed") from e
+        raise ValueError("not a WAV/AIFF file and soundfile is not installed") from e
     x, fs = sf.read(io.BytesIO(data))
     return np.ascontiguousarray(x, dtype=np.float64), int(fs)
 
@@ -104,7 +114,7 @@ def load(source, device: torch.device | str | None = None) -> tuple[torch.Tensor
         torch.device("cuda", torch.cuda.current_device())
     data = read_bytes(source)
     try:
-        info = parse_wav(data)
+        info = parse_audio(data)
     except ValueError:
         host, fs = _decode_other(data)
         ch = 1 if host.ndim == 1 else host.shape[1]

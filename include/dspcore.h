@@ -265,11 +265,18 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
  * Loader, replacing dsp_core.py:10-35 (cargar_senal_audio: soundfile read,
  * channel mean, float32, divide by max|x| when > 1e-6):
  *   dsp_wav_parse        HOST: RIFF/WAVE header of an in-memory file (PCM 8/16/
- *                        24/32-bit, IEEE float 32/64, WAVE_FORMAT_EXTENSIBLE);
- *                        no sample is touched;
+ *                        24/32-bit, IEEE float 32/64, G.711 A-law/mu-law,
+ *                        WAVE_FORMAT_EXTENSIBLE); no sample is touched;
+ *   dsp_audio_parse      HOST: the same for RIFF/WAVE and FORM/AIFF or AIFF-C
+ *                        ('NONE'/'twos'/'sowt' PCM, 'fl32'/'fl64', 'ulaw'/
+ *                        'alaw'); `format` then carries DSP_AUDIO_BE for
+ *                        big-endian samples and DSP_AUDIO_S8 for AIFF's
+ *                        signed 8-bit PCM, and `bits` is the stored width
+ *                        (8 for G.711);
  *   dsp_pcm_to_mono_f32  DEVICE: raw interleaved sample bytes [B][ld_bytes] ->
  *                        float32 [B][ld_out]: each sample scaled as soundfile
- *                        returns it (float64: ints / 2^(bits-1), u8 - 128), the
+ *                        returns it (float64: ints / 2^(bits-1), u8 - 128,
+ *                        G.711 expanded to 16-bit linear / 2^15), the
  *                        channel mean in float64 in numpy's summation order,
  *                        rounded to float32 (bit-identical to the reference);
  *   dsp_peak_normalize_f32  DEVICE: per row, peak = max|x| (float32; a NaN
@@ -290,8 +297,12 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
  * ------------------------------------------------------------------------- */
 #define DSP_WAV_PCM 1    /* integer PCM (8-bit unsigned, 16/24/32-bit signed) */
 #define DSP_WAV_FLOAT 3  /* IEEE float, 32 or 64 bits                           */
+#define DSP_WAV_ALAW 6   /* G.711 A-law, one byte per sample (-> 16-bit linear) */
+#define DSP_WAV_ULAW 7   /* G.711 mu-law, one byte per sample                   */
+#define DSP_AUDIO_BE 0x100 /* format flag: big-endian samples (AIFF)           */
+#define DSP_AUDIO_S8 0x200 /* format flag: 8-bit PCM is signed (AIFF)          */
 typedef struct dsp_wav_info {
-  int32_t format;       /* DSP_WAV_PCM or DSP_WAV_FLOAT                  */
+  int32_t format;       /* DSP_WAV_PCM/FLOAT/ALAW/ULAW, | DSP_AUDIO_*    */
   int32_t channels;     /* interleaved channels, 1..128                  */
   int32_t sample_rate;  /* Hz                                            */
   int32_t bits;         /* bits per sample                               */
@@ -301,6 +312,7 @@ typedef struct dsp_wav_info {
 } dsp_wav_info;
 
 int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info);
+int dsp_audio_parse(const uint8_t* file, size_t len, dsp_wav_info* info);
 int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t channels,
                         int64_t B, int64_t frames, int64_t ld_bytes, float* out,
                         int64_t ld_out, void* stream);

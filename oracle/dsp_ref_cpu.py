@@ -21,26 +21,96 @@ BANDS = (("Sub-Bass", 40), ("Bass", 150), ("Low Mids", 1000),
          ("High Mids", 3000), ("Presence", 5000), ("Brilliance", 10000))
 
 
+def _g711_or_aiff(data):
+    """(float64 samples [frames, ch] or [frames], fs) for the inputs scipy's
+    WAV reader does not take: RIFF/WAVE G.711 (format tags 6 A-law, 7 mu-law)
+    and FORM/AIFF, AIFF-C ('NONE'/'twos'/'sowt' PCM, 'fl32'/'fl64',
+    'ulaw'/'alaw').  Restates libsndfile's decoding as soundfile documents it:
+    G.711 expanded to 16-bit linear (audioop's tables = libsndfile's) / 2^15,
+    AIFF PCM as signed big-endian integers / 2^(bits-1).  None otherwise."""
+    import audioop
+    import struct
+
+    def g711(raw, mu):
+        lin = (audioop.ulaw2lin if mu else audioop.alaw2lin)(raw, 2)
+        return np.frombuffer(lin, dtype="<i2").astype(np.float64) / 32768.0
+
+    if data[:4] == b"RIFF" and data[8:12] == b"WAVE":
+        pos, fmt = 12, None
+        while pos + 8 <= len(data):
+            cid, size = data[pos:pos + 4], struct.unpack("<I", data[pos + 4:pos + 8])[0]
+            body = data[pos + 8:pos + 8 + size]
+            if cid == b"fmt ":
+                fmt = struct.unpack("<HHIIHH", body[:16])
+            elif cid == b"data" and fmt is not None:
+                tag, ch, fs = fmt[0], fmt[1], fmt[2]
+                if tag not in (6, 7):
+                    return None
+                x = g711(body[:len(body) // ch * ch], tag == 7)
+                return (x.reshape(-1, ch) if ch > 1 else x), fs
+            pos += 8 + size + (size & 1)
+        return None
+    if data[:4] != b"FORM" or data[8:12] not in (b"AIFF", b"AIFC"):
+        return None
+    pos, comm = 12, None
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], struct.unpack(">I", data[pos + 4:pos + 8])[0]
+        body = data[pos + 8:pos + 8 + size]
+        if cid == b"COMM":
+            ch, frames, bits = struct.unpack(">hIh", body[:8])
+            e = ((body[8] & 0x7F) << 8) | body[9]
+            mant = int.from_bytes(body[10:18], "big")
+            fs = int(mant * 2.0 ** (e - 16383 - 63))
+            comp = body[18:22] if data[8:12] == b"AIFC" else b"NONE"
+            comm = (ch, frames, bits, fs, comp)
+        elif cid == b"SSND" and comm is not None:
+            ch, frames, bits, fs, comp = comm
+            off = struct.unpack(">I", body[:4])[0]
+            raw = body[8 + off:]
+            if comp in (b"ulaw", b"ULAW", b"alaw", b"ALAW"):
+                x = g711(raw[:frames * ch], comp[:1] in (b"u", b"U"))
+            elif comp in (b"fl32", b"FL32", b"fl64", b"FL64"):
+                dt = ">f4" if comp[2:] == b"32" else ">f8"
+                x = np.frombuffer(raw, dtype=dt, count=frames * ch).astype(np.float64)
+            else:
+                w = bits // 8
+                b = np.frombuffer(raw, dtype=np.uint8, count=frames * ch * w).reshape(-1, w)
+                if comp == b"sowt":
+                    b = b[:, ::-1]
+                v = np.zeros(b.shape[0], dtype=np.int64)
+                for k in range(w):
+                    v = (v << 8) | b[:, k]
+                v = np.where(v >= 1 << (bits - 1), v - (1 << bits), v)
+                x = v.astype(np.float64) / float(1 << (bits - 1))
+            return (x.reshape(-1, ch) if ch > 1 else x), fs
+        pos += 8 + size + (size & 1)
+    return None
+
+
 def load_audio(data):
-    """cargar_senal_audio (reference dsp_core.py:10-35) on WAV bytes, with
-    scipy.io.wavfile.read standing in for soundfile (absent here) and
+    """cargar_senal_audio (reference dsp_core.py:10-35) on WAV / AIFF bytes,
+    with scipy.io.wavfile.read standing in for soundfile (absent here) and
     soundfile's documented float64 scaling restated: integer PCM / 2^(bits-1)
     (24-bit arrives as int32 << 8, so / 2^31), unsigned 8-bit (v - 128) / 128,
-    float as stored.  Parity of that scaling is unpinned (no reference audio
-    ships: .MISSING_LARGE_BLOBS); the mean / cast / normalise are the
-    reference's own numpy calls."""
+    float as stored; G.711 and AIFF(-C) through _g711_or_aiff.  Parity of that
+    scaling is unpinned (no reference audio ships: .MISSING_LARGE_BLOBS); the
+    mean / cast / normalise are the reference's own numpy calls."""
     import io
 
     from scipy.io import wavfile
-    fs, raw = wavfile.read(io.BytesIO(data))
-    if raw.dtype == np.uint8:
-        x = (raw.astype(np.float64) - 128.0) / 128.0
-    elif raw.dtype == np.int16:
-        x = raw.astype(np.float64) / 32768.0
-    elif raw.dtype == np.int32:
-        x = raw.astype(np.float64) / 2147483648.0
+    other = _g711_or_aiff(data)
+    if other is not None:
+        x, fs = other
     else:
-        x = raw.astype(np.float64)
+        fs, raw = wavfile.read(io.BytesIO(data))
+        if raw.dtype == np.uint8:
+            x = (raw.astype(np.float64) - 128.0) / 128.0
+        elif raw.dtype == np.int16:
+            x = raw.astype(np.float64) / 32768.0
+        elif raw.dtype == np.int32:
+            x = raw.astype(np.float64) / 2147483648.0
+        else:
+            x = raw.astype(np.float64)
     if len(x.shape) > 1:
         x = x.mean(axis=1)
     x = x.astype(np.float32)

@@ -2,16 +2,16 @@
 // AddressSanitizer + UndefinedBehaviorSanitizer (make -C
 // dsp-audio-project_amd/csrc sanitize; run by tests/test_host_sanitize.py).
 //
-// Nothing here touches a GPU: the library's sources are compiled host-only
-// (--offload-host-only) and only the entry points that never launch are
-// called -- the WAV header parser on a corpus of malformed files (every
-// truncation and several byte corruptions of valid headers, oversized and odd
-// chunk sizes, nonsense fmt fields, random bytes), the playback header writer,
-// and the chain planners (tile tables, tile length, workspace sizes, x-state
-// geometry, Bluestein size) on edge-case geometries and cascades.  Every input
-// buffer is a heap copy of exactly its length, so any read past it is an ASan
-// report.  Invariants of successful parses are checked; exit status 0 means
-// no sanitizer report and no broken invariant.
+// Nothing here touches a GPU: only the entry points that never launch are
+// called -- the WAV and AIFF/AIFF-C header parsers on a corpus of malformed
+// files (every truncation and several byte corruptions of valid headers,
+// oversized and odd chunk sizes, nonsense fmt/COMM fields, 80-bit rates at
+// their edges, random bytes), the playback header writer, and the chain
+// planners (tile tables, tile length, workspace sizes, x-state geometry,
+// Bluestein size) on edge-case geometries and cascades.  Every input buffer is
+// a heap copy of exactly its length, so any read past it is an ASan report.
+// Invariants of successful parses are checked; exit status 0 means no
+// sanitizer report and no broken invariant.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -82,28 +82,87 @@ std::vector<uint8_t> wav(int fmt_tag, int channels, int rate, int bits, size_t p
   return f;
 }
 
-// Parses an exact-size heap copy; checks the invariants of a success.
+void putbe32(std::vector<uint8_t>& v, uint32_t x) {
+  for (int i = 3; i >= 0; --i) v.push_back((uint8_t)(x >> (8 * i)));
+}
+void putbe16(std::vector<uint8_t>& v, uint16_t x) {
+  v.push_back((uint8_t)(x >> 8));
+  v.push_back((uint8_t)x);
+}
+
+// FORM/AIFF (comp null) or FORM/AIFC with compression `comp`; the rate is
+// written as an 80-bit extended (exponent, 64-bit mantissa).
+std::vector<uint8_t> aiff(const char* comp, int channels, uint32_t rate, int bits, uint32_t frames,
+                          size_t payload, uint32_t ssnd_offset, bool extra_chunk) {
+  std::vector<uint8_t> comm;
+  putbe16(comm, (uint16_t)channels);
+  putbe32(comm, frames);
+  putbe16(comm, (uint16_t)bits);
+  int e = 0;
+  while (e < 31 && (rate >> (e + 1))) ++e;
+  putbe16(comm, (uint16_t)(16383 + e));
+  const uint64_t mant = rate ? (uint64_t)rate << (63 - e) : 0;
+  for (int i = 7; i >= 0; --i) comm.push_back((uint8_t)(mant >> (8 * i)));
+  if (comp) {
+    comm.insert(comm.end(), comp, comp + 4);
+    comm.insert(comm.end(), {4, 'n', 'o', 'n', 'e', 0});
+  }
+  std::vector<uint8_t> body;
+  tag(body, comp ? "AIFC" : "AIFF");
+  tag(body, "COMM");
+  putbe32(body, (uint32_t)comm.size());
+  body.insert(body.end(), comm.begin(), comm.end());
+  if (extra_chunk) {
+    tag(body, "NAME");
+    putbe32(body, 3);
+    body.insert(body.end(), {'a', 'b', 'c', 0});
+  }
+  tag(body, "SSND");
+  putbe32(body, (uint32_t)(8 + ssnd_offset + payload));
+  putbe32(body, ssnd_offset);
+  putbe32(body, 0);
+  body.insert(body.end(), ssnd_offset, 0);
+  for (size_t i = 0; i < payload; ++i) body.push_back((uint8_t)(i * 53));
+  std::vector<uint8_t> f;
+  tag(f, "FORM");
+  putbe32(f, (uint32_t)body.size());
+  f.insert(f.end(), body.begin(), body.end());
+  return f;
+}
+
+// Parses an exact-size heap copy with both parsers (dsp_wav_parse and the
+// RIFF-or-FORM dispatcher dsp_audio_parse); checks the invariants of a success.
 void parse(const std::vector<uint8_t>& f) {
   uint8_t* buf = static_cast<uint8_t*>(std::malloc(f.size() ? f.size() : 1));
   if (!f.empty()) std::memcpy(buf, f.data(), f.size());
-  dsp_wav_info info;
-  std::memset(&info, 0xAB, sizeof(info));
-  const int rc = dsp_wav_parse(buf, f.size(), &info);
-  if (rc == DSP_OK) {
-    ++g_parsed;
-    CHECK(info.channels >= 1 && info.channels <= 128, "channels %d", info.channels);
-    CHECK(info.format == DSP_WAV_PCM || info.format == DSP_WAV_FLOAT, "format %d", info.format);
-    CHECK(info.sample_rate > 0, "sample rate %d", info.sample_rate);
-    CHECK(info.data_offset >= 12 && info.data_bytes >= 0 &&
-              (uint64_t)info.data_offset + (uint64_t)info.data_bytes <= f.size(),
-          "data [%lld, +%lld) outside a %zu-byte file", (long long)info.data_offset,
-          (long long)info.data_bytes, f.size());
-    CHECK(info.frames >= 0 && info.frames * (int64_t)info.channels * (info.bits / 8) <= info.data_bytes,
-          "frames %lld", (long long)info.frames);
-  } else {
-    ++g_rejected;
-    CHECK(rc == DSP_EINVAL, "rc %d", rc);
-    CHECK(std::strlen(dsp_last_error()) > 0, "empty error string");
+  for (int which = 0; which < 2; ++which) {
+    dsp_wav_info info;
+    std::memset(&info, 0xAB, sizeof(info));
+    const int rc = which ? dsp_audio_parse(buf, f.size(), &info) : dsp_wav_parse(buf, f.size(), &info);
+    if (rc == DSP_OK) {
+      ++g_parsed;
+      const int base = info.format & 0xFF;
+      CHECK(info.channels >= 1 && info.channels <= 128, "channels %d", info.channels);
+      CHECK((base == DSP_WAV_PCM || base == DSP_WAV_FLOAT || base == DSP_WAV_ALAW ||
+             base == DSP_WAV_ULAW) &&
+                (info.format & ~(0xFF | DSP_AUDIO_BE | DSP_AUDIO_S8)) == 0 &&
+                (which || (info.format & ~0xFF) == 0),
+            "format %#x", info.format);
+      CHECK(info.bits == 8 || info.bits == 16 || info.bits == 24 || info.bits == 32 ||
+                info.bits == 64, "bits %d", info.bits);
+      CHECK(info.sample_rate > 0, "sample rate %d", info.sample_rate);
+      CHECK(info.data_offset >= 12 && info.data_bytes >= 0 &&
+                (uint64_t)info.data_offset + (uint64_t)info.data_bytes <= f.size(),
+            "data [%lld, +%lld) outside a %zu-byte file", (long long)info.data_offset,
+            (long long)info.data_bytes, f.size());
+      CHECK(info.frames >= 0 &&
+                info.frames * (int64_t)info.channels * (info.bits / 8) <= info.data_bytes,
+            "frames %lld", (long long)info.frames);
+    } else {
+      ++g_rejected;
+      CHECK(rc == DSP_EINVAL, "rc %d", rc);
+      CHECK(std::strlen(dsp_last_error()) > 0, "empty error string");
+    }
   }
   std::free(buf);
 }
@@ -254,8 +313,49 @@ void planners() {
 
 }  // namespace
 
+void aiff_corpus() {
+  std::vector<std::vector<uint8_t>> seeds = {
+      aiff(nullptr, 2, 44100, 16, 100, 400, 0, true), aiff(nullptr, 1, 8000, 8, 7, 7, 0, false),
+      aiff("sowt", 2, 48000, 24, 10, 60, 4, false),   aiff("fl32", 1, 96000, 32, 16, 64, 0, true),
+      aiff("FL64", 5, 8000, 64, 2, 80, 0, false),     aiff("ulaw", 2, 8000, 16, 20, 40, 0, false),
+      aiff("ALAW", 1, 11025, 16, 9, 9, 2, true),      aiff("twos", 128, 8000, 32, 2, 1024, 0, false),
+      wav(6, 1, 8000, 8, 31, false, true),            wav(7, 2, 8000, 8, 40, false, false)};
+  for (const auto& s : seeds) {
+    parse(s);
+    for (size_t n = 0; n <= s.size(); ++n) parse(std::vector<uint8_t>(s.begin(), s.begin() + n));
+    for (size_t i = 0; i < s.size() && i < 96; ++i)
+      for (uint8_t v : {0x00, 0x01, 0x7F, 0x80, 0xFF}) {
+        auto m = s;
+        m[i] = v;
+        parse(m);
+      }
+    for (size_t i = 4; i + 4 <= s.size() && i < 96; i += 2)
+      for (uint32_t v : {0u, 1u, 7u, 8u, 18u, 22u, 0x7FFFFFFFu, 0x80000000u, 0xFFFFFFF7u,
+                         0xFFFFFFFFu}) {
+        auto m = s;
+        for (int k = 0; k < 4; ++k) m[i + k] = (uint8_t)(v >> (8 * (3 - k)));
+        parse(m);
+      }
+  }
+  // COMM fields no decoder takes; rates at the 80-bit edges
+  for (int ch : {0, 1, 2, 128, 129, 65535})
+    for (int bits : {0, 1, 8, 12, 16, 24, 32, 64, 65535})
+      for (const char* c : {(const char*)nullptr, "NONE", "sowt", "fl32", "ulaw", "ima4", "\0\0\0\0"})
+        for (uint32_t rate : {0u, 1u, 44100u, 0x7FFFFFFFu, 0xFFFFFFFFu})
+          parse(aiff(c, ch, rate, bits, 3, 24, 0, false));
+  for (int it = 0; it < 20000; ++it) {
+    std::vector<uint8_t> f(rnd() % 200);
+    for (auto& b : f) b = (uint8_t)rnd();
+    if (f.size() >= 12) std::memcpy(f.data(), it & 1 ? "FORM\0\0\0\0AIFF" : "FORM\0\0\0\0AIFC", 12);
+    if (it % 3 == 0 && f.size() >= 20) std::memcpy(f.data() + 12, it % 2 ? "COMM" : "SSND", 4);
+    parse(f);
+  }
+  CHECK(dsp_audio_parse(nullptr, 10, nullptr) == DSP_EINVAL, "null buffer accepted");
+}
+
 int main() {
   wav_corpus();
+  aiff_corpus();
   header_writer();
   planners();
   std::printf("host_fuzz: %ld parsed, %ld rejected, %d failures\n", g_parsed, g_rejected, g_fail);

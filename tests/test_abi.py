@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 27
+    assert len(names) == 28
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -339,3 +339,46 @@ def test_chain_tile_tables_host_only():
     rc, _, key6 = _tables(lib, nbytes, 48000, c6.n_out, t6.ctypes.data, c6.K, 160, 147,
                           c6.c_offset, _lib.sos_pointer(sos5), 6)
     assert rc == 1 and key6 == 0
+
+
+def test_audio_parse_aiff_and_g711_host_only():
+    """dsp_audio_parse: FORM/AIFF and AIFF-C layouts (PCM 8-32 big- and
+    little-endian, fl32/fl64, G.711) and WAV G.711 give the right format word,
+    width, frame count and sample offset without a GPU; WAV still parses."""
+    import numpy as np
+    import audio_files
+    lib = _lib.load()
+    info = _lib.WavInfo()
+    BE, S8 = _lib.DSP_AUDIO_BE, _lib.DSP_AUDIO_S8
+    for name, (f, frames, ch) in audio_files.cases(np.random.default_rng(3)).items():
+        assert lib.dsp_audio_parse(f, len(f), ctypes.byref(info)) == 0, (name, _lib.last_error())
+        assert (info.frames, info.channels) == (frames, ch), name
+        fmt = info.format
+        if name.startswith("aiff s") or "twos" in name or "NONE" in name or "short" in name:
+            assert fmt & 0xFF == _lib.DSP_WAV_PCM and fmt & BE, name
+            assert bool(fmt & S8) == (info.bits == 8), name
+        elif "sowt" in name:
+            assert fmt & 0xFF == _lib.DSP_WAV_PCM and not fmt & BE, name
+        elif "fl32" in name or "FL64" in name:
+            assert fmt == (_lib.DSP_WAV_FLOAT | BE) and info.bits in (32, 64), name
+        else:
+            mu = "ulaw" in name.lower()
+            assert fmt & 0xFF == (_lib.DSP_WAV_ULAW if mu else _lib.DSP_WAV_ALAW), name
+            assert info.bits == 8 and bool(fmt & BE) == name.startswith("aifc"), name
+    f = audio_files.aiff(bytes(16), 1, 44100, 16, b"twos", ssnd_offset=6)
+    assert lib.dsp_audio_parse(f, len(f), ctypes.byref(info)) == 0
+    assert f[info.data_offset - 6 - 16:info.data_offset - 6 - 12] == b"SSND"
+    assert info.sample_rate == 44100 and info.frames == 8
+    f = _wav(1, 2, 44100, 16, bytes(400))
+    assert lib.dsp_audio_parse(f, len(f), ctypes.byref(info)) == 0 and info.frames == 100
+    for bad in (audio_files.aiff(bytes(8), 1, 44100, 16, b"ima4"),    # unsupported codec
+                audio_files.aiff(bytes(8), 1, 44100, 12),             # 12-bit PCM
+                audio_files.aiff(bytes(8), 0, 44100, 16, comm_frames=4),  # no channels
+                b"FORM\0\0\0\x04AIFF",                                # no chunks
+                audio_files.aiff(bytes(8), 1, 44100, 16)[:40]):       # cut inside COMM
+        assert lib.dsp_audio_parse(bad, len(bad), ctypes.byref(info)) == _lib.DSP_EINVAL
+    # a zero rate (80-bit zero) is refused like WAV's
+    z = bytearray(audio_files.aiff(bytes(8), 1, 44100, 16))
+    at = z.index(b"COMM") + 16
+    z[at:at + 10] = bytes(10)
+    assert lib.dsp_audio_parse(bytes(z), len(z), ctypes.byref(info)) == _lib.DSP_EINVAL

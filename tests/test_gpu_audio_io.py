@@ -139,3 +139,19 @@ def test_batches_past_the_grid_row_limit(gpu):
     x = xt.cpu().numpy()
     for b in (0, 65535, 65536, B - 1):
         np.testing.assert_array_equal(x[b], z[b] / np.max(np.abs(z[b])))
+
+
+def test_loader_aiff_and_g711_bitwise(gpu):
+    """AIFF / AIFF-C (big- and little-endian PCM 8-32, fl32/fl64, G.711) and
+    WAV G.711 decode on the device bitwise equal to the oracle (libsndfile's
+    scaling restated; parity unpinned against soundfile itself, which is not
+    installed -- the oracle's reader is pinned on stdlib aifc and the Sun
+    G.711 end points in test_oracle_golden.py)."""
+    import audio_files
+    from modules import dsp_core
+    from oracle import dsp_ref_cpu as orc
+    for name, (f, frames, ch) in audio_files.cases(np.random.default_rng(12)).items():
+        x, fs = dsp_core.cargar_senal_audio(io.BytesIO(f))
+        ref, rfs = orc.load_audio(f)
+        assert fs == rfs and x.dtype == np.float32 and x.shape == (frames,) == ref.shape, name
+        np.testing.assert_array_equal(x, ref, err_msg=name)

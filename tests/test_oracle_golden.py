@@ -111,3 +111,49 @@ def test_chain_exact(tag, fs, L, M, K):
     np.testing.assert_array_equal(z, g[f"{tag}_z"])
     np.testing.assert_array_equal(mag, g[f"{tag}_mag"])
     np.testing.assert_array_equal(orc.spectrum(z, fs_out)[1], g[f"{tag}_mag2048"])
+
+
+def test_oracle_g711_known_answers():
+    """The oracle's G.711 expansion (audioop, the tables libsndfile uses) on the
+    Sun g711.c end points: mu-law 0x00/0x80 -> -/+32124, 0x7F/0xFF -> 0; A-law
+    0x55/0xD5 -> -/+8, 0x2A/0xAA -> -/+32256."""
+    import audio_files
+    from oracle import dsp_ref_cpu as orc
+    x, fs = orc._g711_or_aiff(audio_files.wav_g711([0x00, 0x80, 0x7F, 0xFF], 1, 8000, 7))
+    assert fs == 8000 and (x * 32768).tolist() == [-32124, 32124, 0, 0]
+    x, _ = orc._g711_or_aiff(audio_files.wav_g711([0x55, 0xD5, 0x2A, 0xAA], 1, 8000, 6))
+    assert (x * 32768).tolist() == [-8, 8, -32256, 32256]
+
+
+def test_oracle_aiff_reader_matches_stdlib_aifc():
+    """Pins the oracle's AIFF/AIFF-C reader on what Python's own aifc module
+    decodes (big-endian PCM 8/16/24/32 and the AIFF-C G.711 codecs)."""
+    import io
+    import warnings
+
+    import audio_files
+    from oracle import dsp_ref_cpu as orc
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)
+        import aifc
+    rng = np.random.default_rng(9)
+    for bits in (8, 16, 24, 32):
+        ints = rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), (300, 2))
+        f = audio_files.aiff(audio_files.pcm_be(ints, bits), 2, 44100, bits, extra_chunk=True)
+        x, fs = orc._g711_or_aiff(f)
+        r = aifc.open(io.BytesIO(f))
+        assert (r.getnchannels(), r.getnframes(), r.getframerate()) == (2, 300, fs)
+        raw = np.frombuffer(r.readframes(300), dtype=np.uint8).reshape(-1, bits // 8)
+        v = np.zeros(raw.shape[0], dtype=np.int64)
+        for k in range(bits // 8):
+            v = (v << 8) | raw[:, k]
+        v = np.where(v >= 1 << (bits - 1), v - (1 << bits), v)
+        np.testing.assert_array_equal(v, ints.reshape(-1))
+        np.testing.assert_array_equal(x.reshape(-1), v / float(1 << (bits - 1)))
+    codes = rng.integers(0, 256, 400, dtype=np.uint8).tobytes()
+    for comp in (b"ulaw", b"alaw"):
+        f = audio_files.aiff(codes, 2, 8000, 16, comp)
+        x, _ = orc._g711_or_aiff(f)
+        r = aifc.open(io.BytesIO(f))
+        lin = np.frombuffer(r.readframes(200), dtype="<i2")     # aifc expands to native order
+        np.testing.assert_array_equal(x.reshape(-1), lin / 32768.0)
