@@ -92,6 +92,8 @@ constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
+constexpr int kScanRow = 14;  // doubles per row of the blocked carry scan (12 used)
+constexpr int kScanFloats = 66 * kScanRow * 2;  // its LDS: 64 rows + row 64 + the park row
 
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -123,7 +125,8 @@ struct TileGeo {
   static constexpr int RS = TSUB + 4;                               // staging row stride
   static constexpr int SF = (kWave / 2) * RS;                       // staging (floats)
   static constexpr int CF = (kWave + 1) * kD * 2;                   // scan slots (floats)
-  static constexpr int LDSF = XF > SF ? (XF > CF ? XF : CF) : (SF > CF ? SF : CF);
+  static constexpr int LDSF0 = XF > SF ? (XF > CF ? XF : CF) : (SF > CF ? SF : CF);
+  static constexpr int LDSF = LDSF0 > kScanFloats ? LDSF0 : kScanFloats;
   static_assert(L <= 4, "four branch slots per tap pair row");
   static_assert(qs(TSUB - 1) < W, "");
 };
@@ -185,6 +188,14 @@ struct TileTables {
   // shift s_i = (i M div L) mod 2 + (1 if the class's phase carries q one
   // further, else 0), zero outside the T taps.
   alignas(16) float seqs[kGenClasses][kGenTS][kCtRow];
+  // k_chain_tile with the SRC on the matrix cores (DSP_SRC_MFMA): the tile's
+  // SRC as Y[48 x 64] = H[48 x 80] X[80 x 64] (H: output i's taps at window
+  // offsets, X: lane n's window in column n), the taps scaled by 2^hexp and
+  // split into two float16 planes (hi + lo), as the A operands of
+  // v_mfma_f32_16x16x32_f16 in lane order: Hmf[mt][ks][plane][lane][j] =
+  // H[16 mt + lane % 16][k0(mt) + 32 ks + 8 (lane / 16) + j] (k0 = 8 mt).
+  alignas(16) _Float16 Hmf[3][2][2][64][8];
+  int32_t hexp, pad2;
 };
 
 struct TileArgs {
@@ -228,6 +239,14 @@ __device__ __forceinline__ double shfl_up_f64(double v, int d) {
   const uint64_t u = __double_as_longlong(v);
   const uint32_t lo = __builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)u);
   const uint32_t hi = __builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// ds_bpermute of a double from lane src.
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(u >> 32));
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
@@ -355,7 +374,7 @@ __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * 
 // Steps 2-5 of the tile (file comment) for a wave that holds its y sub-chunk:
 // pass 1, entry state (hand-off) and scan, publish, y out, s = T m, pass 2,
 // z out.  lds: at least staging_floats(TS) floats the wave may overwrite.
-template <int TS>
+template <int TS, bool YST = true>
 __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
                                              float (&y)[TS], int lane, int64_t b, int64_t tile,
                                              int64_t m0) {
@@ -449,6 +468,8 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     for (int k = 0; k < kS; ++k)
       mac2(mt->Dp[0][k], m_in[2 * k], m_in[2 * k + 1], v[2 * k], v[2 * k + 1]);
   }
+#if DSP_SCAN_KS
+  // Kogge-Stone scan over the 64 lanes with ds_bpermute (round 2; A/B build).
   // m_in waits out the scan in LDS (free until the y store), not in 24 VGPRs
   // of every lane at the kernel's register peak.
   double* park = reinterpret_cast<double*>(lds);
@@ -492,9 +513,114 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     store_flag(a.flags + me, 1u);
   }
 
+#else
+  // Blocked scan through LDS.  Rows r = 0..63 take E'_r (row stride kScanRow
+  // doubles: the b128 accesses of 16 lanes hit 16 distinct bank quads); 48
+  // worker lanes, one per (state block k, segment s of 8 rows), run the
+  // segment's local recurrence u <- D u + E' (D = D_k^TSUB, per-lane loads);
+  // a 3-level Kogge-Stone over the 8 segments of a block (ds_bpermute, powers
+  // D^(8 TSUB 2^d) by squaring D^(8 TSUB)) gives each segment its entry state;
+  // each worker reruns its segment from that state and writes v_r to row r + 1,
+  // so row l holds lane l's entry state m_l = v_(l-1) and the park row m_in.
+  // Per lane: 8 + 3 + 8 block steps (76 fp64 FMAs) and 28 b128 LDS + 12
+  // bpermutes, against 6 levels x 12 doubles (144 FMAs, 168 bpermutes).
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  double* rows = reinterpret_cast<double*>(lds);
+  double* park = rows + 65 * kScanRow;
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+  }
+#pragma unroll
+  for (int k = 0; k < kS; ++k)
+    *reinterpret_cast<f64x2*>(rows + lane * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
+  fence();
+  // worker (k, s): lane 16 (s / 2) + 6 (s % 2) + k; lanes 12..15 of each 16 idle
+  const int r16 = lane & 15, odd = r16 >= 6 ? 1 : 0;
+  const bool worker = r16 < 12;
+  const int sg = 2 * (lane >> 4) + odd;
+  const int kb = worker ? r16 - 6 * odd : 0;
+  const __attribute__((address_space(1))) double* Dg =
+      (const __attribute__((address_space(1))) double*)&a.tt->Dp[0][kb][0];
+  const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
+  const f64x2 d0b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 2);
+  f64x2 e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[i] = *reinterpret_cast<const f64x2*>(rows + (8 * sg + i) * kScanRow + 2 * kb);
+  const __attribute__((address_space(1))) double* D8g = Dg + 3 * kS * 4;  // Dp[3][kb]
+  f64x2 p8a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(D8g);
+  f64x2 p8b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(D8g + 2);
+  double u0 = e[0].x, u1 = e[0].y;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, e[i].x));
+    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, e[i].y));
+    u0 = n0;
+    u1 = n1;
+  }
+#pragma unroll
+  for (int lv = 0; lv < 3; ++lv) {
+    const int dd = 1 << lv;
+    const int ss = sg - dd;
+    const int src = ss >= 0 ? 16 * (ss >> 1) + 6 * (ss & 1) + kb : lane;
+    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
+    if (ss >= 0) {
+      u0 = fma(p8a.x, x0, fma(p8a.y, x1, u0));
+      u1 = fma(p8b.x, x0, fma(p8b.y, x1, u1));
+    }
+    if (lv < 2) {  // D^(8 TSUB 2^(lv+1)) = (D^(8 TSUB 2^lv))^2
+      const f64x2 qa = f64x2{fma(p8a.x, p8a.x, p8a.y * p8b.x), fma(p8a.x, p8a.y, p8a.y * p8b.y)};
+      const f64x2 qb = f64x2{fma(p8b.x, p8a.x, p8b.y * p8b.x), fma(p8b.x, p8a.y, p8b.y * p8b.y)};
+      p8a = qa;
+      p8b = qb;
+    }
+  }
+  {
+    const int ss = sg - 1;
+    const int src = ss >= 0 ? 16 * (ss >> 1) + 6 * (ss & 1) + kb : lane;
+    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
+    u0 = ss >= 0 ? x0 : 0.0;
+    u1 = ss >= 0 ? x1 : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, e[i].x));
+    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, e[i].y));
+    u0 = n0;
+    u1 = n1;
+    if (worker) *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * kb) = f64x2{u0, u1};
+  }
+  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)
+  if (tile + 1 < a.ntiles) {
+    const int64_t me = b * a.ntiles + tile;
+    if (worker && sg == 7) {
+      store_state(a.states + me * kD + 2 * kb, u0);
+      store_state(a.states + me * kD + 2 * kb + 1, u1);
+    }
+#if DSP_HANDOFF_FENCED
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (lane == 16 * 3 + 6) store_flag(a.flags + me, 1u);
+  }
+  fence();
+  double m[kD];
+  {
+    const double* src = lane == 0 ? park : rows + lane * kScanRow;
+#pragma unroll
+    for (int k = 0; k < kS; ++k) {
+      const f64x2 t = *reinterpret_cast<const f64x2*>(src + 2 * k);
+      m[2 * k] = t.x;
+      m[2 * k + 1] = t.y;
+    }
+  }
+  fence();
+#endif  // DSP_SCAN_KS
+
   // ---- 5. y out (unless the caller passed y = NULL), DF2 entry state
   // s = T m, pass 2, z out
-  if (a.y) {
+  if (YST && a.y) {
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
         a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
 #if DSP_DIRECT_STORE
@@ -553,6 +679,157 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #endif
 }
 
+#if DSP_SRC_MFMA
+// ---------------------------------------------------------------------------
+// SRC on the matrix cores (A/B build, -DDSP_SRC_MFMA=1).  Y[48 x 64] = H X
+// per tile as 3 (M) x 4 (N) x 2 (K) v_mfma_f32_16x16x32_f16 tiles, each
+// operand split into float16 hi + lo (x scaled by a power of two per wave so
+// that max|x| lands in [2^14, 2^15), the taps by 2^hexp on the host) and the
+// four products lo*lo, lo*hi, hi*lo, hi*hi accumulated in float32: the split
+// keeps 22 of float32's 24 bits per operand, the error of the sums is that of
+// float32 FMAs (tools/sim_split.py).  x goes to LDS once as the two planes
+// (16-B chunks XOR-swizzled: the B-operand reads of 16 lanes hit 16 distinct
+// bank quads); the result tiles are transposed through the same LDS into the
+// y store's staging rows, from which every lane also takes its 48 outputs.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+constexpr int kMfWin = 32 * 63 + 16 + 64;       // window samples the B operands read
+constexpr int kMfPlane = (kMfWin / 8 + 15) / 16 * 16 * 8;  // halfs per plane (whole swizzle groups)
+__device__ __forceinline__ int mf_chunk(int c) { return c ^ ((c >> 4) & 3); }
+
+template <class GEO>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
+    TileArgs a) {
+  constexpr int TS = GEO::TSUB;
+  static_assert(TS == 48 && GEO::L == 3 && GEO::M == 2, "matrix-core SRC: the L3/M2 tile");
+  static_assert(staging_floats(TS) * 4 <= 2 * kMfPlane * 2 && kScanFloats <= kMfPlane,
+                "staging and scan rows fit the planes");
+  __shared__ __attribute__((aligned(16))) float lds[kMfPlane];  // 2 planes of kMfPlane halfs
+  const int lane = threadIdx.x;
+  const int64_t id = blockIdx.x;
+  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
+  const int64_t m0 = tile * GEO::TILE;
+  const tt_ptr mt = (tt_ptr)a.tt;
+  char* const pl0 = reinterpret_cast<char*>(lds);
+  char* const pl1 = pl0 + kMfPlane * 2;
+
+  // ---- x window -> registers, wave max|x|, split into f16 planes in LDS
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);
+    constexpr int NF = kMfWin / 4;
+    constexpr int NK = (NF + kWave - 1) / kWave;
+    f32x4 v[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int f = lane + kWave * k;
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, kStream);
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      mx = fmaxf(fmaxf(fmaxf(mx, fabsf(v[k].x)), fmaxf(fabsf(v[k].y), fabsf(v[k].z))), fabsf(v[k].w));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    const int ex = (int)((__float_as_uint(mx) >> 23) & 255);
+    int sx = (ex == 0 || ex == 255) ? 0 : 141 - ex;  // max|x| * 2^sx in [2^14, 2^15)
+    sx = __builtin_amdgcn_readfirstlane(sx < -100 ? -100 : (sx > 100 ? 100 : sx));
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int f = lane + kWave * k;
+      if ((k + 1) * kWave <= NF || f < NF) {
+        const float x0 = __builtin_ldexpf(v[k].x, sx), x1 = __builtin_ldexpf(v[k].y, sx);
+        const float x2 = __builtin_ldexpf(v[k].z, sx), x3 = __builtin_ldexpf(v[k].w, sx);
+        const f16x2 h01 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(x0, x1));
+        const f16x2 h23 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(x2, x3));
+        const f16x2 l01 = __builtin_bit_cast(
+            f16x2, __builtin_amdgcn_cvt_pkrtz(x0 - (float)h01.x, x1 - (float)h01.y));
+        const f16x2 l23 = __builtin_bit_cast(
+            f16x2, __builtin_amdgcn_cvt_pkrtz(x2 - (float)h23.x, x3 - (float)h23.y));
+        const int off = (mf_chunk(f >> 1) << 4) + ((f & 1) << 3);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2*>(pl0 + off) =
+            u32x2{__builtin_bit_cast(unsigned int, h01), __builtin_bit_cast(unsigned int, h23)};
+        *reinterpret_cast<u32x2*>(pl1 + off) =
+            u32x2{__builtin_bit_cast(unsigned int, l01), __builtin_bit_cast(unsigned int, l23)};
+      }
+    }
+    fence();
+    // ---- 1. SRC: 12 result tiles of 16 outputs x 16 sub-chunks
+    f32x4 acc[3][4];
+    const f16x8* Ag = reinterpret_cast<const f16x8*>(&a.tt->Hmf[0][0][0][0][0]);
+    const int la = lane & 15, lb = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      f16x8 A[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) A[ks][p] = Ag[((m * 2 + ks) * 2 + p) * kWave + lane];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int chunk = (32 * (16 * n + la) + 8 * m + 32 * ks + 8 * lb) >> 3;
+          const int off = mf_chunk(chunk) << 4;
+          const f16x8 Bh = *reinterpret_cast<const f16x8*>(pl0 + off);
+          const f16x8 Bl = *reinterpret_cast<const f16x8*>(pl1 + off);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][1], Bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][1], Bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][0], Bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][0], Bh, c, 0, 0, 0);
+        }
+        const int sc = -(sx + mt->hexp);
+        acc[m][n] = f32x4{__builtin_ldexpf(c.x, sc), __builtin_ldexpf(c.y, sc),
+                          __builtin_ldexpf(c.z, sc), __builtin_ldexpf(c.w, sc)};
+      }
+    }
+    fence();
+    // ---- y out and every lane's 48 outputs: per half of the sub-chunks, the
+    // tiles go to the staging rows (row = sub-chunk, stride TS + 4), the half
+    // leaves as coalesced float4s, and its lanes read their rows back.
+    float y[TS];
+    constexpr int RS = TS + 4;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int n = 2 * h; n < 2 * h + 2; ++n)
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+          *reinterpret_cast<f32x4*>(lds + (16 * (n - 2 * h) + la) * RS + 16 * m + 4 * lb) = acc[m][n];
+      fence();
+      if (a.y) {
+#pragma unroll
+        for (int k = 0; k < (kWave / 2) * TS / 4 / kWave; ++k) {
+          const int g = 4 * (lane + kWave * k);
+          const int r = g / TS, cc = g - r * TS;
+          const f32x4 f = *reinterpret_cast<const f32x4*>(lds + r * RS + cc);
+          const int64_t off = (m0 + (int64_t)h * (kWave / 2) * TS + g) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), ry, (int)off, 0, kStream);
+        }
+      }
+      if ((lane >> 5) == h) {
+#pragma unroll
+        for (int k = 0; k < TS / 4; ++k) {
+          const f32x4 f = *reinterpret_cast<const f32x4*>(lds + (lane & 31) * RS + 4 * k);
+          y[4 * k] = f.x;
+          y[4 * k + 1] = f.y;
+          y[4 * k + 2] = f.z;
+          y[4 * k + 3] = f.w;
+        }
+      }
+      fence();
+    }
+    pin(y);
+    tile_cascade<TS, false>(a, mt, lds, y, lane, b, tile, m0);
+  }
+}
+#else
 template <class GEO>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
@@ -598,6 +875,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   }
   tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
 }
+
+#endif  // DSP_SRC_MFMA
 
 // ---------------------------------------------------------------------------
 // Generic single-pass kernel: any L, M with ceil(K/L) <= 8 (config 5's
@@ -850,7 +1129,7 @@ struct TilePlan {
 int gen_window(int L, int M, int T) {
   const int64_t w = ((int64_t)(kGenTile - 1) * M) / L + T + 4 + (kGenTT - T) + 2;
   const int64_t r = (w + 3) / 4 * 4;
-  return (int)std::max<int64_t>(r, staging_floats(kGenTS));
+  return (int)std::max<int64_t>(r, std::max(staging_floats(kGenTS), kScanFloats));
 }
 
 size_t gen_lds_bytes(int win) {
@@ -937,7 +1216,7 @@ uint64_t tables_key(const TilePlan& tp, int64_t n_in, int64_t n_out, int K, int 
       h *= 1099511628211ull;
     }
   };
-  const int64_t v[] = {2 /* table layout version */, tp.kind, tp.tsub, n_in, n_out, K, L, M, c, S,
+  const int64_t v[] = {3 /* table layout version */, tp.kind, tp.tsub, n_in, n_out, K, L, M, c, S,
                        (int64_t)sizeof(TileTables)};
   mix(v, sizeof(v));
   if (S > 0 && sos) mix(sos, sizeof(double) * 5 * (size_t)S);
@@ -1190,6 +1469,46 @@ void tap_pairs(const float* taps, int K, TileTables* tt) {
       }
 }
 
+template <class GEO>
+constexpr bool mfma_rows_fit() {
+  for (int i = 0; i < GEO::TSUB; ++i)
+    if (GEO::qs(i) < 8 * (i / 16) || GEO::qs(i) + 2 * GEO::NP > 8 * (i / 16) + 64) return false;
+  return true;
+}
+
+// A operands of the matrix-core SRC (TileTables::Hmf, file comment of the
+// DSP_SRC_MFMA kernel) from the tap pairs: H[i][qs(i) + 2p + e] = TP[p][phi(i)][e],
+// scaled by 2^hexp (max|H| in [2^14, 2^15)) and split into float16 hi + lo.
+template <class GEO>
+void mfma_taps(TileTables* tt) {
+  constexpr int KW = 80;  // window offsets k0(2) + 64
+  static_assert(GEO::TSUB == 48 && GEO::W <= KW, "three 16-row tiles over 80 window samples");
+  static_assert(mfma_rows_fit<GEO>(), "every row of tile m reads window offsets [8 m, 8 m + 64)");
+  std::vector<double> H((size_t)GEO::TSUB * KW, 0.0);
+  double mx = 0.0;
+  for (int i = 0; i < GEO::TSUB; ++i)
+    for (int p = 0; p < GEO::NP; ++p)
+      for (int e = 0; e < 2; ++e) {
+        const double v = tt->TP[p][GEO::phi(i)][e];
+        H[(size_t)i * KW + GEO::qs(i) + 2 * p + e] = v;
+        mx = std::max(mx, std::fabs(v));
+      }
+  int ex = 0;
+  if (mx > 0.0) std::frexp(mx, &ex);  // mx in [2^(ex-1), 2^ex)
+  tt->hexp = 15 - ex;
+  for (int m = 0; m < 3; ++m) {
+    for (int ks = 0; ks < 2; ++ks)
+      for (int lane = 0; lane < kWave; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int row = 16 * m + (lane & 15), col = 8 * m + 32 * ks + 8 * (lane >> 4) + j;
+          const double h = std::ldexp(H[(size_t)row * KW + col], tt->hexp);
+          const _Float16 hi = (_Float16)h;
+          tt->Hmf[m][ks][0][lane][j] = hi;
+          tt->Hmf[m][ks][1][lane][j] = (_Float16)(h - (double)hi);
+        }
+  }
+}
+
 // Class tables of the generic kernel (TileTables::seq / adv).
 void gen_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables* tt) {
   const int T = (K + L - 1) / L, C = gen_classes(L, M);
@@ -1276,8 +1595,10 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   TileTables* tt = static_cast<TileTables*>(out);
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
-  if (tp.kind == 1) tap_pairs<Geo3241>(taps, K, tt);
-  else gen_sequences(taps, K, L, M, c, tt);
+  if (tp.kind == 1) {
+    tap_pairs<Geo3241>(taps, K, tt);
+    mfma_taps<Geo3241>(tt);
+  } else gen_sequences(taps, K, L, M, c, tt);
   if (tp.kind == 3) ct_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}

@@ -7,7 +7,7 @@ objects of the in-tree build.  Time them with tools/gpu_libs.sh.
 
 NOSRC   y = window samples (no SRC FMAs)     NOP1  no pass-1 sums (the float32
         input-normal sums; the float64 change of basis stays)
-NOSCAN  no carry scan                        NOP2  no pass-2 cascade
+NOSCAN  no carry recurrences                       NOP2  no pass-2 cascade
 NOYST   no y store                           NOZST no z store (also lets the
         compiler drop most of pass 2: read it together with NOP2)
 """
@@ -42,9 +42,13 @@ def patched() -> str:
     rep("#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {",
         "#ifdef V_NOP1\n#pragma unroll\n    for (int d = 0; d < kD; ++d) e2[d] = f32x2{y[d], y[d + 1]};\n"
         "    if (false)\n#endif\n#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {")
-    rep("#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {",
-        "#ifndef V_NOSCAN\n#pragma unroll\n  for (int lv = 0; lv < 6; ++lv) {")
-    rep("  // Entry state of the lane's sub-chunk", "#endif\n  // Entry state of the lane's sub-chunk")
+    # carry (round-3 blocked scan): keep the LDS rows, drop the recurrences and
+    # the segment Kogge-Stone (rows get E' as is)
+    rep("  double u0 = e[0].x, u1 = e[0].y;\n", "  double u0 = e[0].x, u1 = e[0].y;\n#ifndef V_NOSCAN\n")
+    rep("  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)\n",
+        "#else\n  if (worker)\n    for (int i = 0; i < 8; ++i)\n"
+        "      *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * kb) = e[i];\n#endif\n"
+        "  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)\n")
     rep("    store_tile<TS>(lds, y, lane, ry, m0);\n",
         "#ifndef V_NOYST\n    store_tile<TS>(lds, y, lane, ry, m0);\n#endif\n")
     rep("  {\n    double pend[kS];",
