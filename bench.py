@@ -38,7 +38,9 @@ numpy/scipy calls as the reference's dsp_core.py -- on a bounded channel
 sample with one process per usable host core, measured BEFORE the GPU is
 initialised), `config3` and `config5` (the other two batched configs on one
 GPU), `host_inclusive` (numpy in, H2D, chain, D2H of y/z/|X|, numpy out) and
-`copy_ceiling`.  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
+`copy_ceiling` and `mix_ceiling` (the HBM rate of streaming kernels with the
+chain kernel's 1 read : 2 writes mix, tools/ubench_rw_mix in a child
+process; roofline.frac_vs_mix_ceiling).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
 (tests of the rank launcher and sharding on CPU).
 """
 from __future__ import annotations
@@ -46,6 +48,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -233,21 +236,25 @@ def kernel_bytes(chain, name):
 
 
 def valu_work(chain, mean_ms):
-    """float64 FMA work of the single-pass kernel, the
-    resource that binds it: per output sample 12 (pass 1) + 24 (pass 2), plus
-    the per-tile carry per TS-sample sub-chunk (6 scan levels x 24, s = T m 72,
-    the entry state 24 = 240 per lane).  None for the two-launch chain."""
+    """float64 FMA work of the single-pass kernel: per output
+    sample 24 (pass 2), plus per TS-sample sub-chunk the carry's 246 (Q e 78,
+    s = T m 60, the blocked scan 28 + 12 + 12 + 32, the entry state 24; static
+    ISA count of k_chain_tile: 1382 per 48-sample lane).  Pass 1 and the SRC
+    are float32 (v_pk_fma_f32).  None for the two-launch chain."""
     ts = chain.tile_len
     if not ts:
         return None
-    per_sample = 36 + 240 / ts
+    per_sample = 24 + 246 / ts
     fma = per_sample * chain.B * chain.n_out
     tflops = 2 * fma / (mean_ms * 1e-3) / 1e12
-    return {"bound": "valu (fp64 FMA issue)", "fp64_fma_per_output_sample": round(per_sample, 3),
+    return {"bound": "valu (fp64 FMA issue) under the power limit",
+            "fp64_fma_per_output_sample": round(per_sample, 3),
             "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
-            "note": "the kernel also issues 21 (L3/M2) or 4 (generic) v_pk_fma_f32 per sample for "
-                    "the SRC; profiles/r02_chain_ablation.txt: ~83 % VALU issue efficiency"}
+            "note": "beside the fp64 FMAs the kernel issues 27 (L3/M2) or 10 (generic) "
+                    "v_pk_fma_f32 per sample (SRC + pass 1); at config 4 it runs at an effective "
+                    "1.70 GHz (GRBM_GUI_ACTIVE / 8 / time, DVFS) against 2.4 GHz peak "
+                    "(DESIGN.md §3.0.2)"}
 
 
 def load_traffic(wl_name, channels):
@@ -415,6 +422,25 @@ def copy_ceiling(device, nbytes=1 << 30, reps=20):
                    f"mean of {reps} after 3 warm, CUDA events"}
 
 
+def mix_ceiling():
+    """HBM ceiling for the chain kernel's traffic mix (1 read : 2 writes: x in,
+    y and z out), measured by tools/ubench_rw_mix (streaming float4 kernels with
+    the chain's nt cache policy, best of three grid sizes) in a child process;
+    None when the binary is absent (built by __graft_entry__.build())."""
+    exe = os.path.join(ROOT, "tools", "ubench_rw_mix")
+    if not os.access(exe, os.X_OK):
+        return None
+    try:
+        out = subprocess.run([exe, "--json"], capture_output=True, text=True, timeout=120,
+                             check=True).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return None
+    return {"value": d["r1w2_gbs"], "unit": "GB/s", "copy_1r1w_gbs": d["r1w1_gbs"],
+            "how": "tools/ubench_rw_mix: nt float4 streams, 1 GiB each, 1 read : 2 writes "
+                   "(the chain kernel's x : y, z), best of grids 4096/16384/65536 x 256"}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
@@ -510,7 +536,9 @@ def main(argv=None):
             torch.cuda.empty_cache()
         extras["host_inclusive"] = host_inclusive(device)
         extras["copy_ceiling"] = copy_ceiling(device)
+        extras["mix_ceiling"] = mix_ceiling()
     ceiling = (extras.get("copy_ceiling") or {}).get("value")
+    mix = (extras.get("mix_ceiling") or {}).get("value")
 
     if rank == 0:
         out = {
@@ -544,6 +572,8 @@ def main(argv=None):
                 "traffic_source": traffic_src if traffic else None,
                 "copy_ceiling_gbs": ceiling,
                 "frac_vs_copy_ceiling": round(achieved / ceiling, 4) if ceiling else None,
+                "mix_ceiling_gbs": mix,
+                "frac_vs_mix_ceiling": round(achieved / mix, 4) if mix else None,
                 "algorithmic_bytes": dom_bytes,
                 "mean_ms": mean_ms,
                 "valu": valu,
@@ -558,6 +588,7 @@ def main(argv=None):
             **{k: extras.get(k) for k in ("config3", "config4", "config5") if k in extras},
             "host_inclusive": extras.get("host_inclusive"),
             "copy_ceiling": extras.get("copy_ceiling"),
+            "mix_ceiling": extras.get("mix_ceiling"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
