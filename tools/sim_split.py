@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Accuracy model of the matrix-core SRC variant (-DDSP_SRC_MFMA=1,
+csrc/chain_tile.hip): config 3's SRC (L3/M2, K121) computed as float32 FMAs
+(the default kernel), as float16 hi + lo operand splits with four products
+(x and taps scaled by powers of two) and as bfloat16 three-way splits with six
+products, each accumulated in float32, against float64; then z after the
+reference EQ at the config-3 gains and at all +15 dB.
+
+    python tools/sim_split.py
+"""
+import numpy as np, sys
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'dsp-audio-project_amd'), ROOT]
+from oracle import dsp_ref_cpu as orc
+from dspcore import design
+rng=np.random.default_rng(1)
+n=6000
+x = rng.uniform(-1,1,n).astype(np.float32)
+p = design.src_plan(n, 48000, 2, 3)
+L,M,K,c = p.L,p.M,p.K,p.c_offset
+h32 = p.taps.astype(np.float32)
+# index lists: y[m] = sum_k h[k] * xe[m*M + c - k], xe[j] = x[j/L] if j%L==0
+nout = p.n_out
+m = np.arange(nout)
+terms_h=[]; terms_x=[]
+for k in range(K):
+    j = m*M + c - k
+    valid = (j % L == 0) & (j >= 0) & (j//L < n)
+    xi = np.where(valid, x[np.clip(j//L,0,n-1)], 0).astype(np.float32)
+    terms_h.append(h32[k]); terms_x.append(xi)
+X = np.stack(terms_x)          # K x nout
+H = np.array(terms_h)          # K
+y64 = (H.astype(np.float64)[:,None]*X.astype(np.float64)).sum(0)
+def acc32(prods):
+    a = np.zeros(prods.shape[1], np.float32)
+    for r in prods: a = (a.astype(np.float64) + r).astype(np.float32)
+    return a
+# (a) fp32 FMA sequential (fused: product exact, one rounding per add)
+ya = acc32(H.astype(np.float64)[:,None]*X.astype(np.float64))
+def split_bf16(v, planes):
+    out=[]; r=v.astype(np.float32)
+    for _ in range(planes):
+        u = r.view(np.uint32) & np.uint32(0xFFFF0000)
+        hi = u.view(np.float32)
+        out.append(hi); r = (r - hi).astype(np.float32)
+    return out
+def split_f16(v, planes):
+    out=[]; r=v.astype(np.float32)
+    for _ in range(planes):
+        hi = r.astype(np.float16).astype(np.float32)
+        out.append(hi); r = (r - hi).astype(np.float32)
+    return out
+hb = split_bf16(H,3); xb = split_bf16(X,3)
+pairs6 = [(1,1),(2,0),(0,2),(1,0),(0,1),(0,0)]
+yc = acc32(np.concatenate([hb[i].astype(np.float64)[:,None]*xb[j].astype(np.float64) for i,j in pairs6]))
+# f16 2-plane with power-of-2 scaling: x by 2^14 (max|x|<=1), taps by 2^10
+sx, sh = 2.0**14, 2.0**10
+hf = split_f16(H*sh,2); xf = split_f16(X*sx,2)
+pairs4 = [(1,1),(1,0),(0,1),(0,0)]
+yb = acc32(np.concatenate([hf[i].astype(np.float64)[:,None]*xf[j].astype(np.float64) for i,j in pairs4])) / (sx*sh)
+for name, yv in [("fp32 fma", ya), ("f16x2 4prod", yb), ("bf16x3 6prod", yc)]:
+    e = np.abs(yv - y64)
+    print(f"{name:14s} max|dy| {e.max():.3e}  rms {np.sqrt((e**2).mean()):.3e}")
+    for gains in [orc.CONFIG3_GAINS, {b:15 for b,_ in orc.BANDS}]:
+        z = orc.equaliser(yv.astype(np.float64), 72000, gains); z0 = orc.equaliser(y64, 72000, gains)
+        print("      z err", f"{np.abs(np.asarray(z)-np.asarray(z0)).max():.3e}")
