@@ -368,6 +368,37 @@ __device__ __forceinline__ void store_direct(const float (&v)[TS], int lane,
   }
 }
 
+// Entry state of the tile: lane 0 waits for the previous tile of the channel
+// (hand-off, file comment) and loads its end state; zero for tile 0 and for
+// the other lanes.
+__device__ __forceinline__ void tile_entry_state(const TileArgs& a, int64_t b, int64_t tile,
+                                                 int lane, double (&m_in)[kD]) {
+#pragma unroll
+  for (int d = 0; d < kD; ++d) m_in[d] = 0.0;
+  if (tile > 0 && lane == 0) {
+    const int64_t prev = b * a.ntiles + tile - 1;
+    uint32_t spins = 0;
+    bool ok = true;
+    while (load_flag(a.flags + prev) == 0u) {
+      if (++spins > a.max_spins) {
+        // Give up: mark the status word; the flag stays for the workspace
+        // reset (a late producer would set it again anyway).
+        store_flag(a.err, 1u);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+#if DSP_HANDOFF_FENCED
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    fence();
+#pragma unroll
+    for (int d = 0; d < kD; ++d) m_in[d] = load_state(a.states + prev * kD + d);
+    if (ok) store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
+  }
+}
+
 // LDS floats store_tile<TS> stages through.
 __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * (ts + 4); }
 
@@ -438,37 +469,16 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // otherwise sink them past it).
   pin(v);
 
-  // ---- 3. entry state of the tile (lane 0), then the scan across the lanes
+  // ---- 3. entry state of the tile and the scan across the lanes
+#if DSP_SCAN_KS
   double m_in[kD];
-#pragma unroll
-  for (int d = 0; d < kD; ++d) m_in[d] = 0.0;
+  tile_entry_state(a, b, tile, lane, m_in);
   if (tile > 0 && lane == 0) {
-    const int64_t prev = b * a.ntiles + tile - 1;
-    uint32_t spins = 0;
-    bool ok = true;
-    while (load_flag(a.flags + prev) == 0u) {
-      if (++spins > a.max_spins) {
-        // Give up: mark the status word; the flag stays for the workspace
-        // reset (a late producer would set it again anyway).
-        store_flag(a.err, 1u);
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-#if DSP_HANDOFF_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-    fence();
-#pragma unroll
-    for (int d = 0; d < kD; ++d) m_in[d] = load_state(a.states + prev * kD + d);
-    if (ok) store_flag(a.flags + prev, 0u);  // consumed: leave the array clear
     // v_0 = D^TSUB m_in + E'_0
 #pragma unroll
     for (int k = 0; k < kS; ++k)
       mac2(mt->Dp[0][k], m_in[2 * k], m_in[2 * k + 1], v[2 * k], v[2 * k + 1]);
   }
-#if DSP_SCAN_KS
   // Kogge-Stone scan over the 64 lanes with ds_bpermute (round 2; A/B build).
   // m_in waits out the scan in LDS (free until the y store), not in 24 VGPRs
   // of every lane at the kernel's register peak.
@@ -527,13 +537,18 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   double* rows = reinterpret_cast<double*>(lds);
   double* park = rows + 65 * kScanRow;
-  if (lane == 0) {
-#pragma unroll
-    for (int d = 0; d < kD; ++d) park[d] = m_in[d];
-  }
 #pragma unroll
   for (int k = 0; k < kS; ++k)
     *reinterpret_cast<f64x2*>(rows + lane * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
+  // The tile's entry state (hand-off wait; lane 0) goes to the park row.
+  {
+    double m_in[kD];
+    tile_entry_state(a, b, tile, lane, m_in);
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+    }
+  }
   fence();
   // worker (k, s): lane 16 (s / 2) + 6 (s % 2) + k; lanes 12..15 of each 16 idle
   const int r16 = lane & 15, odd = r16 >= 6 ? 1 : 0;
@@ -558,6 +573,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     u0 = n0;
     u1 = n1;
   }
+  // m_in (parked above) enters as segment -1: u_0 += D^(8 TSUB) m_in, and
+  // segment 0's entry state is m_in.
+  f64x2 mi = f64x2{0.0, 0.0};
+  if (sg == 0) {
+    mi = *reinterpret_cast<const f64x2*>(park + 2 * kb);
+    u0 = fma(p8a.x, mi.x, fma(p8a.y, mi.y, u0));
+    u1 = fma(p8b.x, mi.x, fma(p8b.y, mi.y, u1));
+  }
 #pragma unroll
   for (int lv = 0; lv < 3; ++lv) {
     const int dd = 1 << lv;
@@ -579,8 +602,8 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     const int ss = sg - 1;
     const int src = ss >= 0 ? 16 * (ss >> 1) + 6 * (ss & 1) + kb : lane;
     const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
-    u0 = ss >= 0 ? x0 : 0.0;
-    u1 = ss >= 0 ? x1 : 0.0;
+    u0 = ss >= 0 ? x0 : mi.x;
+    u1 = ss >= 0 ? x1 : mi.y;
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1673,9 +1696,10 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
     const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
-    if (int rc = allow_lds(k_chain_gct<160, 147>, shm)) return rc;
+    auto kern = k_chain_gct<160, 147>;
+    if (int rc = allow_lds(kern, shm)) return rc;
     TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL((k_chain_gct<160, 147>), dim3((unsigned)(groups * tp.ntiles)),
+    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)),
                        dim3(kWave * kGenWaves), shm, s, a);
   } else {
     DSP_REQUIRE(taps, "null taps");

@@ -212,6 +212,42 @@ def _tables_dtype():
                     align=True)
 
 
+def _table_step(tb, X, u):
+    """One sample of the tables' NORM DF2 realisation (cascade.h): u *= gain;
+    per stage w = u - a1 w1 - a2 w2, v = w + c1 w1 + c2 w2.  State X (12,) in
+    place; returns the output."""
+    cf = tb["cf"]
+    u = u * float(tb["gain"])
+    for k in range(6):
+        c1, c2, a1, a2 = cf[k]
+        w1, w2 = X[2 * k], X[2 * k + 1]
+        w = u - a1 * w1 - a2 * w2
+        v = w + c1 * w1 + c2 * w2
+        X[2 * k + 1], X[2 * k] = w1, w
+        u = v
+    return u
+
+
+def _table_cascade(tb, y):
+    import numpy as np
+    X = np.zeros(12)
+    return np.array([_table_step(tb, X, float(v)) for v in y])
+
+
+def _table_state_space(tb):
+    """(A, B) of the tables' realisation: X' = A X + B u."""
+    import numpy as np
+    A = np.zeros((12, 12))
+    for c in range(12):
+        X = np.zeros(12)
+        X[c] = 1.0
+        _table_step(tb, X, 0.0)
+        A[:, c] = X
+    X = np.zeros(12)
+    _table_step(tb, X, 1.0)
+    return A, X.copy()
+
+
 def _tables(lib, nbytes, *args):
     import numpy as np
     buf = np.zeros(nbytes, np.uint8)
@@ -257,12 +293,18 @@ def test_chain_tile_tables_host_only():
         want = float(tb["TP"][p, (2 * i) % 3, e]) if 0 <= w - qs < 42 else 0.0
         tol = 2.0 ** -21 * abs(want) + 2.0 ** (-24 - int(tb["hexp"]))  # + float16 subnormal step
         assert abs(Hrec[m, ks, lane, j] - want) <= tol, (m, ks, lane, j)
-    # the DF2 realisation pass 2 reads: per stage {b1/b0, b2/b0, a1, a2}, gain prod(b0)
+    # the DF2 realisation pass 2 reads: per stage {b1/b0, b2/b0, a1, a2}, gain
+    # prod(b0); it filters as the reference's cascade does
     rows, gain, norm = design.df2_realization(sos)
     assert norm
     np.testing.assert_array_equal(tb["cf"], rows[:, 1:])
     assert tb["gain"] == gain
-    A, B = design.state_space(sos)
+    from scipy.signal import sosfilt
+    yy = np.random.default_rng(4).uniform(-1, 1, 400)
+    np.testing.assert_allclose(_table_cascade(tb, yy),
+                               sosfilt(np.c_[sos[:, :3], np.ones(6), sos[:, 3:]], yy),
+                               rtol=1e-9, atol=1e-12)
+    A, B = _table_state_space(tb)
     Ti = np.linalg.inv(T)
     for d in range(6):
         D = np.zeros((12, 12))
@@ -311,7 +353,7 @@ def test_chain_tile_tables_host_only():
                            c5.c_offset, _lib.sos_pointer(sos5), 6)
     assert rc == 0 and key5 not in (0, key)
     assert tuple(tb["geo"]) == (32, 0, 160, 147, 1023, 6)
-    A5, B5 = design.state_space(sos5)
+    A5, B5 = _table_state_space(tb)
     y = np.random.default_rng(1).uniform(-1, 1, 32).astype(np.float32)
     X = np.zeros(12)
     for v in y:
