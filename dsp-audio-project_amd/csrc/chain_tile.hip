@@ -550,11 +550,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     }
   }
   fence();
-  // worker (k, s): lane 16 (s / 2) + 6 (s % 2) + k; lanes 12..15 of each 16 idle
-  const int r16 = lane & 15, odd = r16 >= 6 ? 1 : 0;
-  const bool worker = r16 < 12;
-  const int sg = 2 * (lane >> 4) + odd;
-  const int kb = worker ? r16 - 6 * odd : 0;
+  // worker (k, s): lane 8 s + k, k < 6 (lanes 8 s + 6, 8 s + 7 idle; they read
+  // block 0's address, a broadcast).  With this order the b128 row accesses
+  // are free of bank conflicts: a ds_write_b128 group of 8 contiguous lanes is
+  // one segment's 6 blocks, and the ds_read_b128 groups of 16 lanes mix two
+  // segments of each parity on disjoint bank quads (MI355X_MICROARCH.md §LDS).
+  const int sg = lane >> 3;
+  const bool worker = (lane & 7) < 6;
+  const int kb = worker ? (lane & 7) : 0;
   const __attribute__((address_space(1))) double* Dg =
       (const __attribute__((address_space(1))) double*)&a.tt->Dp[0][kb][0];
   const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
@@ -585,7 +588,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   for (int lv = 0; lv < 3; ++lv) {
     const int dd = 1 << lv;
     const int ss = sg - dd;
-    const int src = ss >= 0 ? 16 * (ss >> 1) + 6 * (ss & 1) + kb : lane;
+    const int src = ss >= 0 ? lane - 8 * dd : lane;
     const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
     if (ss >= 0) {
       u0 = fma(p8a.x, x0, fma(p8a.y, x1, u0));
@@ -600,7 +603,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   }
   {
     const int ss = sg - 1;
-    const int src = ss >= 0 ? 16 * (ss >> 1) + 6 * (ss & 1) + kb : lane;
+    const int src = ss >= 0 ? lane - 8 : lane;
     const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
     u0 = ss >= 0 ? x0 : mi.x;
     u1 = ss >= 0 ? x1 : mi.y;
@@ -625,7 +628,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-    if (lane == 16 * 3 + 6) store_flag(a.flags + me, 1u);
+    if (lane == 8 * 7) store_flag(a.flags + me, 1u);
   }
   fence();
   double m[kD];
