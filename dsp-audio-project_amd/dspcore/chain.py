@@ -16,6 +16,7 @@ caller that checks (the default outside graph capture).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -25,6 +26,11 @@ from . import _lib, ops
 from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, max_chunks_for,
                      spectrum_plan, src_plan, xstate_chunk_len)
 
+
+
+# Output row pitch granule in floats (32 = 128 B; DSPCORE_ROW_ALIGN overrides
+# it for A/B timing, any multiple of 4).
+ROW_ALIGN = int(os.environ.get("DSPCORE_ROW_ALIGN", "32"))
 
 class HandoffError(RuntimeError):
     """A single-pass tile hand-off wait gave up: that call's z is wrong
@@ -95,10 +101,11 @@ class Chain:
         self.window = ops._table("hann", self.spec.n_fft, dev)
         self.tw = ops._table("tw", self.spec.n_fft, dev)
         self.sos = np.ascontiguousarray(self.eq.sos, dtype=np.float64)
-        # Rows on 16-byte boundaries (pitch a multiple of 4 floats) so that the
-        # single-pass kernel's float4 stores apply to every n_out; y and z are
-        # [B, n_out] views of the padded buffers.
-        ld = -(-n_out // 4) * 4
+        # Rows on 128-byte boundaries (pitch a multiple of ROW_ALIGN floats): the
+        # single-pass kernel's float4 stores apply to every n_out and its 1-KB
+        # store bursts cover whole cache lines; y and z are [B, n_out] views of
+        # the padded buffers.
+        ld = -(-n_out // ROW_ALIGN) * ROW_ALIGN
         self._ld = ld
         self.keep_y = bool(keep_y)
         self._zbuf = torch.empty((self.B, ld), dtype=torch.float32, device=dev)
