@@ -531,9 +531,11 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // a 3-level Kogge-Stone over the 8 segments of a block (ds_bpermute, powers
   // D^(8 TSUB 2^d) by squaring D^(8 TSUB)) gives each segment its entry state;
   // each worker reruns its segment from that state and writes v_r to row r + 1,
-  // so row l holds lane l's entry state m_l = v_(l-1) and the park row m_in.
-  // Per lane: 8 + 3 + 8 block steps (76 fp64 FMAs) and 28 b128 LDS + 12
-  // bpermutes, against 6 levels x 12 doubles (144 FMAs, 168 bpermutes).
+  // so row l holds lane l's entry state m_l = v_(l-1) and the park row m_in
+  // (the tile's entry state, which enters segment 0 as "segment -1").  Per
+  // lane: 7 + 3 + 8 block steps and two 2x2 squarings (~80 fp64 ops), 29 b128
+  // LDS accesses and 16 bpermutes, against round 2's 6 levels x 12 doubles
+  // (144 FMAs + a 24-FMA entry fold, 168 bpermutes).
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   double* rows = reinterpret_cast<double*>(lds);
   double* park = rows + 65 * kScanRow;
