@@ -5,9 +5,10 @@ race detection / sanitizers on the host C++).
 -fsanitize=address,undefined on the host side (-Xarch_host; device code is
 compiled normally and never launched) and links tests/native/host_fuzz.cpp,
 which feeds the host entry points a malformed-input corpus: every truncation
-and byte/size-field corruption of valid WAV headers, nonsense fmt fields and
-random bytes into dsp_wav_parse (exact-size heap buffers: any over-read is an
-ASan report), extreme arguments into the playback header writer, and edge
+and byte/size-field corruption of valid WAV, AIFF and AIFF-C headers (PCM,
+float, G.711), nonsense fmt/COMM fields, 80-bit rates at their edges and random
+bytes into dsp_wav_parse and dsp_audio_parse (exact-size heap buffers: any
+over-read is an ASan report), extreme arguments into the playback header writer, and edge
 geometries / cascades into the chain planners (tile tables, tile length,
 workspace sizes, x-state geometry, Bluestein and FFT sizes).  No GPU needed.
 __graft_entry__.build() builds the binary; this test builds it if missing.
