@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -51,11 +52,32 @@ double run(const f32x4* in, f32x4* out, long n4, int grid) {
 // --json: one line {"r1w2_gbs": best 1:2 rate over the grids, "r1w1_gbs": ...}
 // (bench.py's ceiling for the chain kernel's mix).
 int main(int argc, char** argv) {
+  // --burn S: the 1 : 2 stream back to back for S seconds (power / clock
+  // readings under a pure HBM load, tools/gpu_power_stream.sh)
+  const bool burn = argc > 2 && argv[1][2] == 'b';
   g_json = argc > 1 && argv[1][0] == '-';
   const long n4 = (1L << 30) / 16;  // 1 GiB per stream
   f32x4 *in, *out;
   if (hipMalloc(&in, 2 * n4 * 16) != hipSuccess || hipMalloc(&out, 2 * n4 * 16) != hipSuccess) return 1;
   (void)hipMemset(in, 0, 2 * n4 * 16);
+  if (burn) {
+    const double secs = atof(argv[2]);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    long launches = 0;
+    for (float ms = 0.f; ms < secs * 1e3f;) {
+      for (int r = 0; r < 200; ++r, ++launches)
+        hipLaunchKernelGGL((k<1, 2>), dim3(65536), dim3(256), 0, 0, in, out, n4, 1.f);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("burn %.1f s %.0f GB/s\n", ms / 1e3, 3.0 * n4 * 16 * launches / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    }
+    return 0;
+  }
   double b12 = 0, b11 = 0;
   for (int grid : {4096, 16384, 65536}) {
     if (!g_json) run<1, 0>(in, out, n4, grid);
