@@ -247,14 +247,14 @@ def valu_work(chain, mean_ms):
     per_sample = 24 + 246 / ts
     fma = per_sample * chain.B * chain.n_out
     tflops = 2 * fma / (mean_ms * 1e-3) / 1e12
-    return {"bound": "valu (fp64 FMA issue) under the power limit",
+    return {"bound": "package power (1400 W cap): fp64 + packed fp32 VALU on top of the HBM stream",
             "fp64_fma_per_output_sample": round(per_sample, 3),
             "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
             "note": "beside the fp64 FMAs the kernel issues 27 (L3/M2) or 10 (generic) "
-                    "v_pk_fma_f32 per sample (SRC + pass 1); at config 4 it runs at an effective "
-                    "1.70 GHz (GRBM_GUI_ACTIVE / 8 / time, DVFS) against 2.4 GHz peak "
-                    "(DESIGN.md §3.0.2)"}
+                    "v_pk_fma_f32 per sample (SRC + pass 1); it runs at the 1400 W package "
+                    "power cap (config 4: sclk ~1.72 GHz of 2.4; a pure 1R:2W HBM stream at "
+                    "5.1 TB/s draws ~865 W), profiles/r03_power_clocks.txt, DESIGN.md §3.0.2"}
 
 
 def load_traffic(wl_name, channels):
