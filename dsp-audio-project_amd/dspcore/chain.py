@@ -55,14 +55,20 @@ class Chain:
     def __init__(self, cfg: ChainConfig, batch: int, device: torch.device | str = "cuda",
                  chunk_len: int | None = None, use_table: bool = True,
                  use_xstate: bool = True, plan_batch: int | None = None,
-                 keep_y: bool = True):
+                 keep_y: bool = True, spectra: tuple = ("z",)):
         """plan_batch: the batch size the cascade's chunking is planned for
         (default: `batch`).  Shards of one job pass the job's total batch so
         that every shard runs the same chunking and the rows come out bitwise
         equal to the unsharded run (design.max_chunks_for).
         keep_y=False: run() returns (None, z, mag) and, where the single-pass
         kernel serves the geometry, y is never written (dsp_chain_f32 with
-        y = NULL); otherwise y lives in an internal buffer."""
+        y = NULL); otherwise y lives in an internal buffer.
+        spectra: which magnitude spectra a run() computes, of "x", "y", "z" (z
+        always: dsp_chain_f32 produces it).  ("x", "y", "z") is app.py:203-205's
+        rerun -- the input's spectrum at fs, the SRC output's and the EQ
+        output's at fs' -- each with calcular_espectro_magnitud's segment rule
+        on the first limit_pts samples; they land in self.mags[which] and
+        self.frequencies(which) gives the rfftfreq axis."""
         ops.require_gpu()
         self.cfg = cfg
         self.B = int(batch)
@@ -148,6 +154,35 @@ class Chain:
             self._ybuf = self.y = None
         self.xtable, self.xrows = (ops.xstate_table(self.sos, self.src, self.chunk_len, dev)
                                    if self.xstate else (None, 0))
+        # Spectra of x and y beside z's (app.py:203-205).
+        which = tuple(spectra)
+        if "z" not in which or not set(which) <= {"x", "y", "z"}:
+            raise ValueError(f"spectra must name 'z' and any of 'x', 'y' (got {which})")
+        if "y" in which and not self.keep_y:
+            raise ValueError("the y spectrum needs keep_y=True")
+        self.spec_plans = {"z": self.spec}
+        self.mags = {"z": self.mag}
+        for w in ("x", "y"):
+            if w in which:
+                n = cfg.n_in if w == "x" else n_out
+                plan = spectrum_plan(n if cfg.limit_pts is None else min(n, cfg.limit_pts),
+                                     cfg.n_fft)
+                self.spec_plans[w] = plan
+                self.mags[w] = torch.empty((self.B, plan.n_fft // 2 + 1), dtype=torch.float32,
+                                           device=dev)
+
+    def frequencies(self, which: str = "z") -> np.ndarray:
+        """rfftfreq axis of spectrum `which` (dsp_core.py:94-98): x at fs, y and
+        z at fs'."""
+        n = self.spec_plans[which].n_fft
+        fs = self.cfg.fs if which == "x" else self.fs_out
+        return np.fft.rfftfreq(n, 1.0 / fs)[: n // 2 + 1]
+
+    def _extra_spectra(self, x: torch.Tensor, y: torch.Tensor | None) -> None:
+        for w, src in (("x", x), ("y", y)):
+            if w in self.mags:
+                p = self.spec_plans[w]
+                ops.spectrum(src, p.seg_start, p.seg_len, p.n_fft, out=self.mags[w])
 
     # -- algorithmic traffic (SURVEY.md §8(d)) ---------------------------------
     def algorithmic_bytes(self) -> int:
@@ -217,6 +252,7 @@ class Chain:
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), stream.cuda_stream)
             _lib.check(rc, "dsp_chain_f32")
+            self._extra_spectra(x, self.y)
             if check is None:
                 check = self.tile_len > 0 and not torch.cuda.is_current_stream_capturing()
             if check:
@@ -249,5 +285,6 @@ class Chain:
         mark(1, 1)
         mark(2, 0)
         ops.spectrum(z, self.spec.seg_start, self.spec.seg_len, self.spec.n_fft, out=self.mag)
+        self._extra_spectra(x, y)
         mark(2, 1)
         return y, z, self.mag

@@ -263,3 +263,38 @@ def test_tables_with_another_key_are_not_used(gpu):
         assert torch.equal(got, w)
     rz = orc.chain(x[0].cpu().numpy(), 48000, 3, 2, gains_b, None, 4096)[1]
     assert np.max(np.abs(z[0].cpu().numpy() - rz)) <= EQ_ATOL
+
+
+def test_chain_app_rerun_spectra_x_y_z(gpu):
+    """Chain(spectra=("x", "y", "z")) is app.py:203-205's rerun: the spectra of
+    the input (at fs), the SRC output and the EQ output (at fs') over the first
+    limit_pts samples, each within 1e-5 max|X| of the oracle's
+    calcular_espectro_magnitud and on its frequency axis; z's spectrum is the
+    chain's own, bitwise the same as without the extras."""
+    import numpy as np
+    import torch
+
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(31)
+    x = rng.uniform(-1, 1, (2, 48000)).astype(np.float32)
+    cfg = ChainConfig(48000, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=2048, limit_pts=100000)
+    ch = Chain(cfg, 2, gpu, spectra=("x", "y", "z"))
+    xt = torch.from_numpy(x).to(gpu)
+    y, z, mag = ch.run(xt)
+    plain = Chain(cfg, 2, gpu)
+    _, _, mag0 = plain.run(xt)
+    assert torch.equal(mag, mag0) and ch.mags["z"] is mag
+    for b in range(2):
+        ry, _ = orc.resample(x[b], 48000, 2, 3)
+        rz = orc.equaliser(ry, 72000, orc.CONFIG3_GAINS)
+        for which, sig, fs in (("x", x[b], 48000), ("y", ry, 72000), ("z", rz, 72000)):
+            f_ref, m_ref = orc.spectrum(np.asarray(sig)[:100000], fs)
+            got = ch.mags[which][b].cpu().numpy()
+            assert got.shape == m_ref.shape, which
+            assert np.max(np.abs(got - m_ref)) <= 1e-5 * np.max(m_ref), which
+            np.testing.assert_allclose(ch.frequencies(which), f_ref, rtol=1e-12, atol=0)
+    with pytest.raises(ValueError):
+        Chain(cfg, 2, gpu, spectra=("x",))
+    with pytest.raises(ValueError):
+        Chain(cfg, 2, gpu, keep_y=False, spectra=("y", "z"))
