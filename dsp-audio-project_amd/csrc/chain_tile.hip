@@ -92,6 +92,11 @@ constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
+// Config 5 (160/147): k_chain_gct; -DDSP_C5_G5=1 builds the class-uniform
+// k_chain_g5 instead (measured 22 % slower).
+#ifndef DSP_C5_G5
+#define DSP_C5_G5 0
+#endif
 constexpr int kScanRow = 14;  // doubles per row of the blocked carry scan (12 used)
 constexpr int kScanFloats = 66 * kScanRow * 2;  // its LDS: 64 rows + row 64 + the park row
 
@@ -402,15 +407,11 @@ __device__ __forceinline__ void tile_entry_state(const TileArgs& a, int64_t b, i
 // LDS floats store_tile<TS> stages through.
 __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * (ts + 4); }
 
-// Steps 2-5 of the tile (file comment) for a wave that holds its y sub-chunk:
-// pass 1, entry state (hand-off) and scan, publish, y out, s = T m, pass 2,
-// z out.  lds: at least staging_floats(TS) floats the wave may overwrite.
-template <int TS, bool YST = true>
-__device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
-                                             float (&y)[TS], int lane, int64_t b, int64_t tile,
-                                             int64_t m0) {
-  // ---- 2. pass 1: zero-state end state of the sub-chunk
-  double v[kD];
+// Pass 1 (file comment, step 2): the sub-chunk's zero-state end state in
+// block-diagonal coordinates, E' = Q sum_i Gc[i] y[i] (float32 sums in
+// input-normal coordinates, one float64 change of basis).
+template <int TS>
+__device__ __forceinline__ void pass1_state(tt_ptr mt, const float (&y)[TS], double (&v)[kD]) {
 #if DSP_P1_F64
   // float64 sums in block-diagonal coordinates (round 2; A/B reference)
 #pragma unroll
@@ -465,6 +466,63 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     }
   }
 #endif
+}
+
+// Pass 2 (file comment, step 5): DF2 entry state s = T m, the cascade rerun
+// over the sub-chunk from it and the clip; y becomes z in place.
+template <int TS>
+__device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, float (&y)[TS],
+                                              const double (&m)[kD]) {
+  // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
+  // rows and columns for padding stages), so row r starts from m[r].
+  double s1[kS], s2[kS];
+#pragma unroll
+  for (int r = 0; r < kD; ++r) {
+    double acc = m[r];
+#pragma unroll
+    for (int cc = 0; cc < (r / 2) * 2; ++cc) acc = fma(mt->T[r][cc], m[cc], acc);
+    if (r & 1) s2[r / 2] = acc;
+    else s1[r / 2] = acc;
+  }
+  // Pass 2, diagonally pipelined: step s runs stage k on sample s - k, so the
+  // six stage updates of a step are independent (six FMA chains in flight
+  // instead of one 24-deep chain per sample).  Per sample and stage the
+  // operations are cascade_step's: the results are bitwise the same.
+  float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
+  // Opaque uniform bounds: otherwise the compiler clips to +-1 and selects the
+  // unclipped value per sample (4 VALU per sample instead of max + min).
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  {
+    double pend[kS];  // pend[k]: stage k's output from the previous step
+#pragma unroll
+    for (int st = 0; st < TS + kS - 1; ++st) {
+#pragma unroll
+      for (int k = kS - 1; k >= 0; --k) {
+        const int t = st - k;
+        if (t < 0 || t >= TS) continue;
+        const double u = k == 0 ? (double)y[t] * mt->gain : pend[k - 1];
+        const double c1 = mt->cf[k][0], c2 = mt->cf[k][1], a1 = mt->cf[k][2], a2 = mt->cf[k][3];
+        const double w = fma(-a2, s2[k], fma(-a1, s1[k], u));
+        const double v2 = fma(c2, s2[k], fma(c1, s1[k], w));
+        s2[k] = s1[k];
+        s1[k] = w;
+        if (k == kS - 1) y[t] = clip_f32((float)v2, lo, hi);
+        else pend[k] = v2;
+      }
+    }
+  }
+}
+
+// Steps 2-5 of the tile (file comment) for a wave that holds its y sub-chunk:
+// pass 1, entry state (hand-off) and scan, publish, y out, s = T m, pass 2,
+// z out.  lds: at least staging_floats(TS) floats the wave may overwrite.
+template <int TS, bool YST = true>
+__device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
+                                             float (&y)[TS], int lane, int64_t b, int64_t tile,
+                                             int64_t m0) {
+  // ---- 2. pass 1: zero-state end state of the sub-chunk
+  double v[kD];
+  pass1_state<TS>(mt, y, v);
   // Keep the SRC and pass 1 ahead of the hand-off wait (the compiler would
   // otherwise sink them past it).
   pin(v);
@@ -658,44 +716,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #endif
   }
   pin(y);
-  // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
-  // rows and columns for padding stages), so row r starts from m[r].
-  double s1[kS], s2[kS];
-#pragma unroll
-  for (int r = 0; r < kD; ++r) {
-    double acc = m[r];
-#pragma unroll
-    for (int cc = 0; cc < (r / 2) * 2; ++cc) acc = fma(mt->T[r][cc], m[cc], acc);
-    if (r & 1) s2[r / 2] = acc;
-    else s1[r / 2] = acc;
-  }
-  // Pass 2, diagonally pipelined: step s runs stage k on sample s - k, so the
-  // six stage updates of a step are independent (six FMA chains in flight
-  // instead of one 24-deep chain per sample).  Per sample and stage the
-  // operations are cascade_step's: the results are bitwise the same.
-  float lo = a.clip ? -1.f : -INFINITY, hi = a.clip ? 1.f : INFINITY;
-  // Opaque uniform bounds: otherwise the compiler clips to +-1 and selects the
-  // unclipped value per sample (4 VALU per sample instead of max + min).
-  asm volatile("" : "+v"(lo), "+v"(hi));
-  {
-    double pend[kS];  // pend[k]: stage k's output from the previous step
-#pragma unroll
-    for (int st = 0; st < TS + kS - 1; ++st) {
-#pragma unroll
-      for (int k = kS - 1; k >= 0; --k) {
-        const int t = st - k;
-        if (t < 0 || t >= TS) continue;
-        const double u = k == 0 ? (double)y[t] * mt->gain : pend[k - 1];
-        const double c1 = mt->cf[k][0], c2 = mt->cf[k][1], a1 = mt->cf[k][2], a2 = mt->cf[k][3];
-        const double w = fma(-a2, s2[k], fma(-a1, s1[k], u));
-        const double v2 = fma(c2, s2[k], fma(c1, s1[k], w));
-        s2[k] = s1[k];
-        s1[k] = w;
-        if (k == kS - 1) y[t] = clip_f32((float)v2, lo, hi);
-        else pend[k] = v2;
-      }
-    }
-  }
+  pass2_cascade<TS>(a, mt, y, m);
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   int lane_z = lane;
@@ -1141,12 +1162,293 @@ k_chain_gct(TileArgs a) {
   tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
 }
 
+
+// ---------------------------------------------------------------------------
+// Config-5 kernel with class-uniform waves (k_chain_g5<L, M>, round 3; an A/B
+// build, -DDSP_C5_G5=1: measured 1.54 vs 1.26 ms for k_chain_gct at config 5,
+// profiles/r03_c5_g5_ab.txt).  Sub-chunks
+// of 32 outputs repeat their polyphase pattern with period C = 5 (the phase
+// classes, k_chain_gen's comment), so a workgroup of C waves takes a tile of
+// 64 C = 320 consecutive sub-chunks (10240 outputs) of one channel and wave w
+// computes the sub-chunks j = 5 l + w of class w: its taps are wave-uniform,
+// read through the scalar cache (no tap rows in LDS), and the five waves share
+// one x window.  SRC (same FMA order as k_chain_gct, so y is bitwise the same)
+// and pass 1 per lane; the carry is the blocked scan over the tile's 320 rows:
+// wave w scans segments 8 w .. 8 w + 7 (as tile_cascade), writes its group
+// total, and after one barrier takes its group's entry state from the totals
+// of the waves before it (<= 4 block steps, D^(64 TSUB) by squaring); the
+// segment entry adds D^(8 TSUB s) of it (Dp[3..5], by the bits of s).  Each
+// wave stages its y and z stores in its own LDS slice (half a wave of rows at
+// a time): one row = one sub-chunk = one 128-byte line.
+// ---------------------------------------------------------------------------
+constexpr int kG5Waves = 5;                               // = phase classes (160/147)
+#ifndef G5_TAPBLK
+#define G5_TAPBLK 1
+#endif
+constexpr int kG5Sub = kWave * kG5Waves;                  // sub-chunks per tile
+constexpr int kG5Tile = kG5Sub * kGenTS;                  // outputs per tile
+constexpr int kG5ScanFloats = ((kG5Sub + 2) * kScanRow + kG5Waves * kD) * 2;
+constexpr int kG5StageFloats = kG5Waves * staging_floats(kGenTS);
+
+// Stores a wave's 64 sub-chunks (lane l: sub-chunk 5 l + w, TS = 32 outputs)
+// through its staging slice: per half of the lanes, rows (stride TS + 4) into
+// LDS, then 8 lanes per row read them back and store the row's 128 bytes.
+__device__ __forceinline__ void g5_store(float* stage, const float (&v)[kGenTS], int lane, int w,
+                                         __amdgpu_buffer_rsrc_t rs, int64_t m0) {
+  constexpr int TS = kGenTS, RS = TS + 4;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    fence();
+    if ((lane >> 5) == h) {
+      float* row = stage + (lane & 31) * RS;
+#pragma unroll
+      for (int k = 0; k < TS / 4; ++k)
+        *reinterpret_cast<float4*>(row + 4 * k) =
+            make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    fence();
+#pragma unroll
+    for (int k = 0; k < (kWave / 2) * TS / 4 / kWave; ++k) {
+      const int g = 4 * (lane + kWave * k);
+      const int r = g / TS, c = g - r * TS;
+      const float4 f = *reinterpret_cast<const float4*>(stage + r * RS + c);
+      u32x4 d;
+      d.x = __float_as_uint(f.x);
+      d.y = __float_as_uint(f.y);
+      d.z = __float_as_uint(f.z);
+      d.w = __float_as_uint(f.w);
+      const int64_t j = (int64_t)kG5Waves * (r + (kWave / 2) * h) + w;
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)((m0 + TS * j + c) * 4), 0, kStream);
+    }
+  }
+  fence();
+}
+
+template <int L, int M>
+__global__ __launch_bounds__(kWave * kG5Waves) __attribute__((amdgpu_waves_per_eu(5))) void
+k_chain_g5(TileArgs a) {
+  static_assert(M < L, "q advances by 0 or 1 per output");
+  constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(1))) double* gdp;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t id = blockIdx.x;
+  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major, one channel per workgroup
+  const int T = a.T;
+  const tt_ptr mt = (tt_ptr)a.tt;
+  const int64_t m0 = tile * kG5Tile;
+  const int j = kG5Waves * lane + w;  // the lane's sub-chunk within the tile (class w)
+
+  // ---- x window of the tile: x[qa .. qa + win) (zeros outside [0, n_in))
+  const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
+  const int64_t qa = (qlo >> 2) << 2;
+  {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int nf = a.win >> 2;
+    for (int f0 = 0; f0 < nf; f0 += 8 * kG5Sub) {
+      f32x4 v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kG5Sub + (int)threadIdx.x;  // past the window: harmless reads
+        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + r * kG5Sub + (int)threadIdx.x;
+        if (f < nf) *reinterpret_cast<f32x4*>(smem + 4 * f) = v[r];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 1. SRC of the lane's 32 outputs; class w's taps from the scalar cache
+  float y[kGenTS];
+  {
+    const int64_t j0 = (m0 + (int64_t)kGenTS * j) * M + a.c;
+    const float* xl = smem + (int)(j0 / L - (T - 1) - qa);
+    f32x2 X[NPW];
+#pragma unroll
+    for (int mm = 0; mm < NPW; ++mm) X[mm] = f32x2{xl[2 * mm], xl[2 * mm + 1]};
+    // one opaque table pointer per G5_TAPBLK outputs: their rows' scalar
+    // loads are issued together (fewer lgkmcnt waits, more SGPRs)
+    tt_ptr tq = mt;
+#pragma unroll
+    for (int i = 0; i < kGenTS; ++i) {
+      if (i % G5_TAPBLK == 0) asm volatile("" : "+s"(tq));
+      const auto* t = &tq->seqs[w][i][0];
+      const int g2 = (i * M / L) / 2;
+      f32x2 acc = {0.f, 0.f};
+      acc = __builtin_elementwise_fma(f32x2{t[0], t[1]}, X[g2], acc);
+      acc = __builtin_elementwise_fma(f32x2{t[2], t[3]}, X[g2 + 1], acc);
+      acc = __builtin_elementwise_fma(f32x2{t[4], t[5]}, X[g2 + 2], acc);
+      acc = __builtin_elementwise_fma(f32x2{t[6], t[7]}, X[g2 + 3], acc);
+      acc = __builtin_elementwise_fma(f32x2{t[8], t[9]}, X[g2 + 4], acc);
+      y[i] = acc.x + acc.y;
+    }
+  }
+  pin(y);
+  __syncthreads();  // the x window is dead: its LDS becomes the scan rows
+
+  // ---- 2. pass 1, rows, the tile's entry state
+  double* rows = reinterpret_cast<double*>(smem);
+  double* park = rows + (kG5Sub + 1) * kScanRow;
+  double* gtot = rows + (kG5Sub + 2) * kScanRow;  // [wave][12] group totals
+  {
+    double v[kD];
+    pass1_state<kGenTS>(mt, y, v);
+    pin(v);
+#pragma unroll
+    for (int k = 0; k < kS; ++k)
+      *reinterpret_cast<f64x2*>(rows + j * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
+  }
+  if (w == 0) {
+    double m_in[kD];
+    tile_entry_state(a, b, tile, lane, m_in);
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. blocked scan over the tile's 320 rows (tile_cascade's, per wave
+  // on its group of 64 rows, plus the group carry between the waves)
+  const int sg = lane >> 3;
+  const bool worker = (lane & 7) < 6;
+  const int kb = worker ? (lane & 7) : 0;
+  const int r0 = kWave * w + 8 * sg;  // the segment's first row
+  const gdp Dg = (gdp)&a.tt->Dp[0][kb][0];
+  const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
+  const f64x2 d0b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 2);
+  f64x2 p8a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 3 * kS * 4);
+  f64x2 p8b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 3 * kS * 4 + 2);
+  double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f64x2 ei = *reinterpret_cast<const f64x2*>(rows + (r0 + i) * kScanRow + 2 * kb);
+    if (i == 0) {
+      u0 = ei.x;
+      u1 = ei.y;
+      continue;
+    }
+    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, ei.x));
+    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, ei.y));
+    u0 = n0;
+    u1 = n1;
+  }
+  f64x2 mi = f64x2{0.0, 0.0};  // entry of the wave's first segment (m_in for wave 0)
+  if (w == 0 && sg == 0) {
+    mi = *reinterpret_cast<const f64x2*>(park + 2 * kb);
+    u0 = fma(p8a.x, mi.x, fma(p8a.y, mi.y, u0));
+    u1 = fma(p8b.x, mi.x, fma(p8b.y, mi.y, u1));
+  }
+#pragma unroll
+  for (int lv = 0; lv < 3; ++lv) {
+    const int dd = 1 << lv;
+    const int ss = sg - dd;
+    const int src = ss >= 0 ? lane - 8 * dd : lane;
+    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
+    if (ss >= 0) {
+      u0 = fma(p8a.x, x0, fma(p8a.y, x1, u0));
+      u1 = fma(p8b.x, x0, fma(p8b.y, x1, u1));
+    }
+    // D^(8 TSUB 2^(lv+1)); after the loop p8 = D^(64 TSUB), the group step
+    const f64x2 qa2 = f64x2{fma(p8a.x, p8a.x, p8a.y * p8b.x), fma(p8a.x, p8a.y, p8a.y * p8b.y)};
+    const f64x2 qb2 = f64x2{fma(p8b.x, p8a.x, p8b.y * p8b.x), fma(p8b.x, p8a.y, p8b.y * p8b.y)};
+    p8a = qa2;
+    p8b = qb2;
+  }
+  if (worker && sg == 7) *reinterpret_cast<f64x2*>(gtot + w * kD + 2 * kb) = f64x2{u0, u1};
+  {
+    const int ss = sg - 1;
+    const int src = ss >= 0 ? lane - 8 : lane;
+    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
+    u0 = ss >= 0 ? x0 : mi.x;
+    u1 = ss >= 0 ? x1 : mi.y;
+  }
+  __syncthreads();  // group totals
+  if (w > 0) {
+    // entry of group w: P = sum over the groups before it, P <- D^(64 TSUB) P + G
+    f64x2 P = *reinterpret_cast<const f64x2*>(gtot + 2 * kb);
+    for (int g = 1; g < w; ++g) {
+      const f64x2 G = *reinterpret_cast<const f64x2*>(gtot + g * kD + 2 * kb);
+      P = f64x2{fma(p8a.x, P.x, fma(p8a.y, P.y, G.x)), fma(p8b.x, P.x, fma(p8b.y, P.y, G.y))};
+    }
+    // ... carried to the segment's start: D^(8 TSUB sg) P by the bits of sg
+#pragma unroll
+    for (int bit = 0; bit < 3; ++bit) {
+      if ((sg >> bit) & 1) {
+        const gdp Db = Dg + (3 + bit) * kS * 4;
+        const f64x2 ra = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Db);
+        const f64x2 rb = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Db + 2);
+        P = f64x2{fma(ra.x, P.x, ra.y * P.y), fma(rb.x, P.x, rb.y * P.y)};
+      }
+    }
+    u0 += P.x;
+    u1 += P.y;
+  }
+  // rerun the segment from its entry state, in place: each worker reads its
+  // block of row r (E'_r) and overwrites it with v_r; no other lane or wave
+  // touches that block (so row j - 1 holds sub-chunk j's entry state)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f64x2* rp = reinterpret_cast<f64x2*>(rows + (r0 + i) * kScanRow + 2 * kb);
+    const f64x2 ei = *rp;
+    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, ei.x));
+    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, ei.y));
+    u0 = n0;
+    u1 = n1;
+    if (worker) *rp = f64x2{u0, u1};
+  }
+  // ---- 4. publish the tile's end state (the last wave's segment-7 workers)
+  if (w == kG5Waves - 1 && tile + 1 < a.ntiles) {
+    const int64_t me = b * a.ntiles + tile;
+    if (worker && sg == 7) {
+      store_state(a.states + me * kD + 2 * kb, u0);
+      store_state(a.states + me * kD + 2 * kb + 1, u1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 8 * 7) store_flag(a.flags + me, 1u);
+  }
+  __syncthreads();  // rows complete
+  double m[kD];
+  {
+    const double* src = j == 0 ? park : rows + (j - 1) * kScanRow;
+#pragma unroll
+    for (int k = 0; k < kS; ++k) {
+      const f64x2 t = *reinterpret_cast<const f64x2*>(src + 2 * k);
+      m[2 * k] = t.x;
+      m[2 * k + 1] = t.y;
+    }
+  }
+  __syncthreads();  // every lane has its entry state: the staging may overwrite the rows
+
+  // ---- 5. y out, pass 2, z out (each wave through its own staging slice)
+  float* stage = smem + w * staging_floats(kGenTS);
+  if (a.y) {
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+    g5_store(stage, y, lane, w, ry, m0);
+  }
+  pin(y);
+  pass2_cascade<kGenTS>(a, mt, y, m);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+      a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+  int lane_z = lane;
+  asm volatile("" : "+v"(lane_z));
+  g5_store(stage, y, lane_z, w, rz, m0);
+}
+
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
 typedef TileGeo<3, 2, 41, 0> Geo3241;
 
 struct TilePlan {
-  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen, 3: k_chain_gct<160, 147>
+  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen, 3: k_chain_gct<160, 147>, 4: k_chain_g5<160, 147>
   int64_t tsub, tile, ntiles;
   int win;   // kind 2: floats of a wave's x window
 };
@@ -1181,6 +1483,18 @@ int gen_classes(int L, int M) {
 }
 constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
 
+// x window of a k_chain_g5 tile (as gen_window for 10240 outputs, +4 for the
+// shifted class rows' reach) and the kernel's LDS: the window, later the scan
+// rows, later the five staging slices.
+int g5_window(int L, int M, int T) {
+  const int64_t w = ((int64_t)(kG5Tile - 1) * M) / L + T + 4 + (kGenTT - T) + 2 + 4;
+  return (int)((w + 3) / 4 * 4);
+}
+
+size_t g5_lds_bytes(int win) {
+  return (size_t)std::max(win, std::max(kG5ScanFloats, kG5StageFloats)) * sizeof(float);
+}
+
 size_t ct_lds_bytes(int classes, int win) {
   return ((size_t)classes * kCtClassStride + (size_t)kGenWaves * win) * sizeof(float);
 }
@@ -1201,6 +1515,17 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
     tp->ntiles = ceil_div(n_out, tp->tile);
     tp->win = 0;
     return true;
+  }
+  if (DSP_C5_G5 && L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) == kG5Waves) {
+    const int win = g5_window(L, M, TT);
+    if (g5_lds_bytes(win) <= kGenLdsMax) {
+      tp->kind = 4;
+      tp->tsub = kGenTS;
+      tp->tile = kG5Tile;
+      tp->ntiles = ceil_div(n_out, tp->tile);
+      tp->win = win;
+      return true;
+    }
   }
   if (L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
     // Window pairs up to (31 M div L) rounded to even + 10 past the lane's
@@ -1627,7 +1952,7 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
     tap_pairs<Geo3241>(taps, K, tt);
     mfma_taps<Geo3241>(tt);
   } else gen_sequences(taps, K, L, M, c, tt);
-  if (tp.kind == 3) ct_sequences(taps, K, L, M, c, tt);
+  if (tp.kind == 3 || tp.kind == 4) ct_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
     tt->cf[k][0] = p.c[k][1];
@@ -1697,6 +2022,12 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,
                        a);
+  } else if (tp.kind == 4) {
+    const size_t shm = g5_lds_bytes(tp.win);
+    auto kern = k_chain_g5<160, 147>;
+    if (int rc = allow_lds(kern, shm)) return rc;
+    TraceScope trace("chain_tile", s);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave * kG5Waves), shm, s, a);
   } else if (tp.kind == 3) {
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
