@@ -49,6 +49,23 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
   return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
 }
 
+// |v|.  sqrtf is correctly rounded, which the compiler expands around
+// v_sqrt_f32 into ~14 instructions (denormal scaling and a two-sided fma
+// correction); the bare instruction is within 1 ulp, 2^-23 relative, far inside
+// the spectra's 1e-5 tolerance, and drops ~450 of the ~2900 VALU instructions
+// a 4096-point magnitude spectrum takes per wave.  -DDSP_MAG_CR=1: sqrtf.
+#ifndef DSP_MAG_CR
+#define DSP_MAG_CR 0
+#endif
+__device__ __forceinline__ float cabsf_(float2 v) {
+  const float p = fmaf(v.x, v.x, v.y * v.y);
+#if DSP_MAG_CR
+  return sqrtf(p);
+#else
+  return __builtin_amdgcn_sqrtf(p);
+#endif
+}
+
 // a * W_16^q for a compile-time q (after unrolling); exact for q % 4 == 0.
 __device__ __forceinline__ float2 w16mul(float2 a, int q) {
   constexpr float c1 = 0.92387953251128674f;  // cos(pi/8)
@@ -194,7 +211,7 @@ __device__ __forceinline__ void store_output(const FftArgs& a, int64_t t, int k,
                                              bool live) {
   if (!live) return;
   if constexpr (MODE == kSpec) {
-    if (k <= N / 2) a.out[t * a.ld_out + k] = sqrtf(fmaf(v.x, v.x, v.y * v.y));
+    if (k <= N / 2) a.out[t * a.ld_out + k] = cabsf_(v);
   } else {
     reinterpret_cast<float2*>(a.out)[t * a.ld_out + k] = v;
   }
@@ -390,8 +407,8 @@ __global__ __launch_bounds__(Plan<LOG2N - 1>::NT) void k_spec_real(FftArgs a) {
     const float2 w = a.tw[k < NH ? k : 0];  // k = NH/2 < N/2 always; table holds W_N^k, k < N/2
     const float2 wo = cmul(o, w);
     const float2 xk = cadd(e, wo), xm = csub(e, wo);
-    mr[k] = sqrtf(fmaf(xk.x, xk.x, xk.y * xk.y));
-    if (k > 0 && k < NH / 2) mr[NH - k] = sqrtf(fmaf(xm.x, xm.x, xm.y * xm.y));
+    mr[k] = cabsf_(xk);
+    if (k > 0 && k < NH / 2) mr[NH - k] = cabsf_(xm);
     if (k == 0) mr[NH] = fabsf(zk.x - zk.y);
   }
 }
@@ -483,7 +500,11 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
   using PL = typename SS::PL;
   constexpr int NH = SS::NH, R0 = SS::R0, NB0 = SS::NB0, NQ = SS::NQ;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  const int tl = threadIdx.x / PL::TPT;
+  int tl = threadIdx.x / PL::TPT;
+  // A transform of >= 64 threads is whole waves: tl is wave-uniform, and saying
+  // so keeps the frame's buffer resource in SGPRs (otherwise every buffer load
+  // sits in a readfirstlane waterfall loop).
+  if constexpr (PL::TPT % 64 == 0) tl = __builtin_amdgcn_readfirstlane(tl);
   const int j0 = threadIdx.x - tl * PL::TPT;
   float2* buf = lds + tl * PL::PADN;
   f32x4_t raw[NQ][R0];
@@ -552,8 +573,8 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
         const float2 w = twp[k < NH ? k : 0];
         const float2 wo = cmul(o, w);
         const float2 xk = cadd(e, wo), xm = csub(e, wo);
-        mr[k] = sqrtf(fmaf(xk.x, xk.x, xk.y * xk.y));
-        if (k > 0 && k < NH / 2) mr[NH - k] = sqrtf(fmaf(xm.x, xm.x, xm.y * xm.y));
+        mr[k] = cabsf_(xk);
+        if (k > 0 && k < NH / 2) mr[NH - k] = cabsf_(xm);
         if (k == 0) mr[NH] = fabsf(zk.x - zk.y);
       }
     }
@@ -686,7 +707,7 @@ __global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(
     const int64_t k = r0 + c + NA * k1;
     const float2 v = lds[c * TS + lpad(k1)];
     if constexpr (MODE == kSpec) {
-      if (k <= f.N / 2) a.out[b * a.ld_out + k] = sqrtf(fmaf(v.x, v.x, v.y * v.y));
+      if (k <= f.N / 2) a.out[b * a.ld_out + k] = cabsf_(v);
     } else {
       reinterpret_cast<float2*>(a.out)[b * a.ld_out + k] = v;
     }
