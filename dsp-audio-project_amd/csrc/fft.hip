@@ -49,6 +49,60 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
   return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
 }
 
+// Complex values as 2-float vectors: every add, product and fma below is one
+// v_pk_*_f32 (a complex product is a pk_mul and a pk_fma with operand
+// swizzles), half the VALU instructions of the float2-struct code.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pf2 pcmul(pf2 a, pf2 w) { return a.xx * w + a.yy * pf2{-w.y, w.x}; }
+__device__ __forceinline__ pf2 pmi(pf2 a) { return pf2{a.y, -a.x}; }  // a * (-i)
+
+// The same with register operands, spelled out: the compiler builds the
+// swapped, negated copy of w ({-w.y, w.x}) with a move and an xor, where the
+// VOP3P operand selects and negations do it for free.
+//   a * w:      t = (a.x w.x, a.x w.y);  r = t + (-a.y w.y, a.y w.x)
+//   s + d * w:  the same with s as the first accumulator
+//   t -+ i d:   (t.x +- d.y, t.y -+ d.x)  (t + (-i) d and t - (-i) d)
+__device__ __forceinline__ pf2 vcmul(pf2 a, pf2 w) {
+  pf2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+__device__ __forceinline__ pf2 vcfma(pf2 d, pf2 w, pf2 s) {
+  pf2 t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(d), "v"(w), "v"(s));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(d), "v"(w), "v"(t));
+  return r;
+}
+__device__ __forceinline__ pf2 vadd_mi(pf2 t, pf2 d) {
+  pf2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+  return r;
+}
+__device__ __forceinline__ pf2 vsub_mi(pf2 t, pf2 d) {
+  pf2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+  return r;
+}
+
+
+// Variable-twiddle products and the radix-4 butterfly through the packed
+// helpers above (-DDSP_FFT_ASM=0: the float2 expressions).
+#ifndef DSP_FFT_ASM
+#define DSP_FFT_ASM 1
+#endif
+__device__ __forceinline__ float2 cmulv(float2 a, float2 w) {
+#if DSP_FFT_ASM
+  const pf2 r = vcmul(pf2{a.x, a.y}, pf2{w.x, w.y});
+  return make_float2(r.x, r.y);
+#else
+  return cmul(a, w);
+#endif
+}
+
 // |v|.  sqrtf is correctly rounded, which the compiler expands around
 // v_sqrt_f32 into ~14 instructions (denormal scaling and a two-sided fma
 // correction); the bare instruction is within 1 ulp, 2^-23 relative, far inside
@@ -94,11 +148,18 @@ __device__ __forceinline__ float2 w16mul(float2 a, int q) {
 __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
   const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
   const float2 t2 = cadd(a1, a3), d = csub(a1, a3);
-  const float2 t3 = make_float2(d.y, -d.x);  // (a1 - a3) * (-i)
   a0 = cadd(t0, t2);
-  a1 = cadd(t1, t3);
   a2 = csub(t0, t2);
+#if DSP_FFT_ASM
+  const pf2 r1 = vadd_mi(pf2{t1.x, t1.y}, pf2{d.x, d.y});  // t1 + (a1 - a3) * (-i)
+  const pf2 r3 = vsub_mi(pf2{t1.x, t1.y}, pf2{d.x, d.y});
+  a1 = make_float2(r1.x, r1.y);
+  a3 = make_float2(r3.x, r3.y);
+#else
+  const float2 t3 = make_float2(d.y, -d.x);  // (a1 - a3) * (-i)
+  a1 = cadd(t1, t3);
   a3 = csub(t1, t3);
+#endif
 }
 
 // In-place forward DFT of R points, natural order in and out.
@@ -291,16 +352,16 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
       float2 w[R];
       w[1] = tw.w[b];
 #pragma unroll
-      for (int r = 2; r < R; ++r) w[r] = (r & 1) ? cmul(w[r - 1], w[1]) : cmul(w[r / 2], w[r / 2]);
+      for (int r = 2; r < R; ++r) w[r] = (r & 1) ? cmulv(w[r - 1], w[1]) : cmulv(w[r / 2], w[r / 2]);
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[r]);
+      for (int r = 1; r < R; ++r) v[b][r] = cmulv(v[b][r], w[r]);
     } else if constexpr (NS > 1) {
       // Few live registers: w1, w2, w4, w8 by squaring, w_r as the product of
       // the powers in r's binary digits, applied as soon as it is formed.
       float2 p2[4];
       p2[0] = tw.w[b];
 #pragma unroll
-      for (int e = 1; e < 4; ++e) p2[e] = cmul(p2[e - 1], p2[e - 1]);
+      for (int e = 1; e < 4; ++e) p2[e] = cmulv(p2[e - 1], p2[e - 1]);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         float2 w = make_float2(1.f, 0.f);
@@ -308,10 +369,10 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if ((r >> e) & 1) {
-            w = first ? p2[e] : cmul(w, p2[e]);
+            w = first ? p2[e] : cmulv(w, p2[e]);
             first = false;
           }
-        v[b][r] = cmul(v[b][r], w);
+        v[b][r] = cmulv(v[b][r], w);
       }
     }
     dft<R>(v[b]);
@@ -405,7 +466,7 @@ __global__ __launch_bounds__(Plan<LOG2N - 1>::NT) void k_spec_real(FftArgs a) {
     const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
     const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
     const float2 w = a.tw[k < NH ? k : 0];  // k = NH/2 < N/2 always; table holds W_N^k, k < N/2
-    const float2 wo = cmul(o, w);
+    const float2 wo = cmulv(o, w);
     const float2 xk = cadd(e, wo), xm = csub(e, wo);
     mr[k] = cabsf_(xk);
     if (k > 0 && k < NH / 2) mr[NH - k] = cabsf_(xm);
@@ -571,7 +632,7 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
         const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
         const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
         const float2 w = twp[k < NH ? k : 0];
-        const float2 wo = cmul(o, w);
+        const float2 wo = cmulv(o, w);
         const float2 xk = cadd(e, wo), xm = csub(e, wo);
         mr[k] = cabsf_(xk);
         if (k > 0 && k < NH / 2) mr[NH - k] = cabsf_(xm);
@@ -618,6 +679,272 @@ int launch_spec_stream(const FftArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// One-wave 4096-point magnitude spectrum (round 3; the default for log2n = 12,
+// the benchmark's n_fft; -DDSP_SPEC_WAVE=0 keeps k_spec_stream).  A wave owns
+// one transform at a time and never waits on another wave: the 2048 packed
+// values c[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] sit 32 per lane and the
+// 2048-point transform is a 32 x 64 four-step split
+//   n = 64 n1 + n2 (lane n2 holds n1 = 0..31),   k = k1 + 32 k2
+//   A  B[n2][k1] = W_2048^(n2 k1) DFT32_n1(c[64 n1 + n2])         registers
+//   T  lane L = 2 k1 + h takes Y[k1][2m + h], m < 32                LDS, 2 planes of 8 KB
+//   B  F_h[j] = DFT32_m(...);  Z[k1 + 32 j] = F_0 + W_64^j F_1,
+//      Z[k1 + 32 (j + 32)] = F_0 - W_64^j F_1                        registers + DPP pair swap
+// so lane L ends with Z[K], K = k1 + 1024 h + 32 j (j < 32).  The real split
+//   X[K] = s - i W_4096^K d,  s = Z[K] + conj Z[-K],  d = Z[K] - conj Z[-K]
+// (with Z already halved: the 1/2 rides on the step-A twiddles) takes Z[-K]
+// from lane (1 - L) mod 64, register 31 - j, by one bpermute per component;
+// lanes 0 and 1, each other's partners at register 32 - j, take the previous
+// bpermute's value (and their own Z at j = 0).  For fixed j, |X[K]| is two runs
+// of 32 consecutive floats across the wave.  Per transform and lane: 32 sample
+// + 32 window + 32 twiddle loads, 128 LDS accesses, 64 bpermutes, 64 DPP moves,
+// 32 stores, no barrier: k_spec_stream's three LDS Stockham passes need a
+// workgroup barrier each and more instructions, and that kernel is
+// issue-bound.
+// ---------------------------------------------------------------------------
+// W_N^m for any m from the table exp(-2 pi i k / N), k < N/2.
+__device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
+  m &= N - 1;
+  const float2 w = tw[m < N / 2 ? m : m - N / 2];
+  return m < N / 2 ? w : make_float2(-w.x, -w.y);
+}
+
+#ifndef DSP_SPEC_WAVE
+#define DSP_SPEC_WAVE 0
+#endif
+#ifndef DSP_SPEC_WAVE_OCC
+#define DSP_SPEC_WAVE_OCC 2  // waves per SIMD k_spec_wave12 is compiled for
+#endif
+constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
+constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
+constexpr int kWavePerGroup = 4;
+
+// W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).
+__device__ __forceinline__ pf2 w128(int j) {
+  constexpr float c[33] = {
+      1.000000000e+00f, 9.987954562e-01f, 9.951847267e-01f, 9.891765100e-01f,
+      9.807852804e-01f, 9.700312532e-01f, 9.569403357e-01f, 9.415440652e-01f,
+      9.238795325e-01f, 9.039892931e-01f, 8.819212643e-01f, 8.577286100e-01f,
+      8.314696123e-01f, 8.032075315e-01f, 7.730104534e-01f, 7.409511254e-01f,
+      7.071067812e-01f, 6.715589548e-01f, 6.343932842e-01f, 5.956993045e-01f,
+      5.555702330e-01f, 5.141027442e-01f, 4.713967368e-01f, 4.275550934e-01f,
+      3.826834324e-01f, 3.368898534e-01f, 2.902846773e-01f, 2.429801799e-01f,
+      1.950903220e-01f, 1.467304745e-01f, 9.801714033e-02f, 4.906767433e-02f,
+      0.0f};  // cos(pi j / 64)
+  const float sgn = j < 64 ? 1.f : -1.f;  // W_128^(j+64) = -W_128^j
+  j &= 63;
+  const float cs = j <= 32 ? c[j] : -c[64 - j];
+  const float sn = j <= 32 ? c[32 - j] : c[j - 32];
+  return pf2{sgn * cs, -sgn * sn};
+}
+
+// a * W_128^j for a compile-time j; exact for multiples of 32.
+__device__ __forceinline__ pf2 pw128(pf2 a, int j) {
+  j &= 127;
+  if (j == 0) return a;
+  if (j == 32) return pmi(a);
+  if (j == 64) return -a;
+  if (j == 96) return -pmi(a);
+  return pcmul(a, w128(j));
+}
+
+__device__ __forceinline__ void pdft4(pf2& a0, pf2& a1, pf2& a2, pf2& a3) {
+  const pf2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
+  a0 = t0 + t2;
+  a1 = vadd_mi(t1, d);
+  a2 = t0 - t2;
+  a3 = vsub_mi(t1, d);
+}
+
+// In-place 16- and 32-point DFTs, natural order in and out (dft<16>'s 4 x 4
+// split; 32 = 2 x 16 with a radix-2 combine).
+__device__ __forceinline__ void pdft16(pf2 (&v)[16]) {
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) pdft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+#pragma unroll
+  for (int k1 = 1; k1 < 4; ++k1)
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2) v[4 * k1 + n2] = pw128(v[4 * k1 + n2], 8 * n2 * k1);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) pdft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+  pf2 o[16];
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) o[k1 + 4 * k2] = v[4 * k1 + k2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+
+__device__ __forceinline__ void pdft32(pf2 (&v)[32]) {
+  pf2 e[16], o[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    e[i] = v[2 * i];
+    o[i] = v[2 * i + 1];
+  }
+  pdft16(e);
+  pdft16(o);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const pf2 t = pw128(o[k], 4 * k);
+    v[k] = e[k] + t;
+    v[k + 16] = e[k] - t;
+  }
+}
+
+// Orders this wave's LDS accesses (they execute in order within a wave; this
+// keeps the compiler from moving them across the exchange).
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float swap_pair(float v) {  // the value of lane L ^ 1
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float bperm(int addr, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// Frame t's samples, lane's pairs (x[128 n1 + 2 lane], x[128 n1 + 2 lane + 1]),
+// through a raw buffer resource over the frame: samples past the frame's valid
+// range read as zeros (the zero padding of dsp_core.py:81-82).
+__device__ __forceinline__ void wave_frame_load(const FftArgs& a, int64_t t, int lane,
+                                                u32x2_t (&raw)[32]) {
+  constexpr int N = 4096;
+  const InRow ir = in_row<kSpec>(a, t);
+  const int64_t valid = ir.valid < N ? (ir.valid > 0 ? ir.valid : 0) : N;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.in) + ir.base, 0, (int)(valid * 4), 0x00020000);
+#pragma unroll
+  for (int n1 = 0; n1 < 32; ++n1)
+    raw[n1] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * lane, 512 * n1, 2);
+}
+
+__global__ __launch_bounds__(64 * kWavePerGroup)
+__attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVE_OCC))) void k_spec_wave12(FftArgs a) {
+  constexpr int N = 4096, NH = 2048;
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the window, once per workgroup (LDS latency instead of an L2 round trip
+  // per transform), then one transpose buffer per wave
+  for (int i = threadIdx.x; i < N / 4; i += 64 * kWavePerGroup)
+    reinterpret_cast<f32x4_t*>(ldsf)[i] = reinterpret_cast<const f32x4_t*>(a.win)[i];
+  __syncthreads();
+  const pf2* wl0 = reinterpret_cast<const pf2*>(ldsf);
+  float* buf = ldsf + N + wv * kWaveLds;
+  const int hi = lane & 1, k1 = lane >> 1;
+  const int rd = k1 * kWaveRow + hi;        // transpose read base
+  const int src = ((1 - lane) & 63) << 2;   // bpermute address of Z[-K]'s lane
+  const int K0 = k1 + 1024 * hi;
+  const float sg = hi ? -1.f : 1.f;
+  const pf2* twp = reinterpret_cast<const pf2*>(a.tw);
+  const pf2 wl = twp[2 * lane];             // W_2048^lane
+  const pf2 wb = twp[K0];                   // W_4096^K0
+  pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const int m = (16 * lane * k) & (N - 1);
+    w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
+  }
+  const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
+  int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv;
+  // the frame in flight: transform t + nw's samples load while t computes
+  u32x2_t raw[32];
+  if (t < a.B) wave_frame_load(a, t, lane, raw);
+  for (; t < a.B; t += nw) {
+    // an opaque per-iteration copy of the lane's parity: the combine's 31
+    // per-lane twiddles below are loop-invariant, and hoisting them would
+    // hold 62 VGPRs
+    float hf = (float)hi;
+    asm volatile("" : "+v"(hf));
+    const pf2 hh = pf2{hf, hf};
+    // (and of the window's address: its 32 LDS reads would be hoisted too)
+    int z0 = 0;
+    asm volatile("" : "+s"(z0));
+    const pf2* win = wl0 + z0;
+    pf2 v[32];
+#pragma unroll
+    for (int n1 = 0; n1 < 32; ++n1)
+      v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} *
+              win[64 * n1 + lane];
+    if (t + nw < a.B) wave_frame_load(a, t + nw, lane, raw);
+    // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
+    // powers come from the table every 8 steps and by products in between)
+    pdft32(v);
+    {
+      pf2 p = 0.5f * wl;
+      v[0] *= 0.5f;
+#pragma unroll
+      for (int k = 1; k < 32; ++k) {
+        if (k % 8 == 0) {
+          p = w8[k / 8 - 1];
+        } else if (k > 1) {
+          p = vcmul(p, wl);
+        }
+        v[k] = vcmul(v[k], p);
+      }
+    }
+    // T: Y[k1][n2] -> lane 2 k1 + h reads Y[k1][2m + h], one plane at a time
+    wave_lds_order();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + lane] = v[k].x;
+    wave_lds_order();
+#pragma unroll
+    for (int m = 0; m < 32; ++m) v[m].x = buf[rd + 2 * m];
+    wave_lds_order();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + lane] = v[k].y;
+    wave_lds_order();
+#pragma unroll
+    for (int m = 0; m < 32; ++m) v[m].y = buf[rd + 2 * m];
+    // B: DFT over m, then the radix-2 step across the lane pair: lane h = 1
+    // scales its F_1 by W_64^j, the pair swaps, and Z = own * (+-1) + other
+    pdft32(v);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      pf2 u = v[j];
+      if (j > 0) {
+        const pf2 one = pf2{1.f, 0.f};
+        u = vcmul(u, one + hh * (w128(2 * j) - one));  // h ? W_64^j : 1
+      }
+      v[j] = u * sg + pf2{swap_pair(u.x), swap_pair(u.y)};
+    }
+    // real split and |X[K]|; W_4096^K = W_4096^K0 W_128^j
+    float* mr = a.out + t * a.ld_out;
+    pf2 prev = v[0];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const pf2 q = pf2{bperm(src, v[31 - j].x), bperm(src, v[31 - j].y)};
+      const pf2 zm = lane < 2 ? prev : q;
+      prev = q;
+      const pf2 zk = v[j];
+      const pf2 sm = pf2{zk.x + zm.x, zk.y - zm.y};
+      const pf2 d = pf2{zk.x - zm.x, zk.y + zm.y};
+      const pf2 x = vcfma(d, pw128(wb, j + 32), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
+      mr[K0 + 32 * j] = cabsf_(make_float2(x.x, x.y));
+    }
+    if (lane == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
+  }
+}
+
+int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
+  if (int rc = allow_lds(k_spec_wave12, shm)) return rc;
+  const int64_t groups = ceil_div(a.B, kWavePerGroup);
+  const int res = resident_groups(k_spec_wave12, 64 * kWavePerGroup, shm);
+  DSP_REQUIRE(res > 0, "occupancy query failed");
+  const unsigned grid = (unsigned)(groups < res ? groups : res);
+  hipLaunchKernelGGL(k_spec_wave12, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
+  DSP_LAUNCHED("k_spec_wave12");
+  return DSP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Four-step FFT for N = 2^15 .. 2^DSP_MAX_LOG2N_FFT (beyond one workgroup's
 // LDS): N = NA * NB, n = n1 + NB n2, k = k2 + NA k1 (n1, k1 < NB; n2, k2 < NA)
 //   step A: Y[n1][k2] = W_N^(n1 k2) * sum_n2 x[n1 + NB n2] W_NA^(n2 k2)
@@ -638,12 +965,6 @@ constexpr int kCols = 8;
 // (N + N/16 + 1) complex values within 160 KB of LDS.
 __host__ __device__ constexpr int kcols_for(int log2) {
   return log2 <= 11 ? kCols : log2 == 12 ? 4 : log2 == 13 ? 2 : 1;
-}
-
-__device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
-  m &= N - 1;
-  const float2 w = tw[m < N / 2 ? m : m - N / 2];
-  return m < N / 2 ? w : make_float2(-w.x, -w.y);
 }
 
 struct Fft4Args {
@@ -764,7 +1085,7 @@ int dispatch_spec(const FftArgs& a, int log2n, hipStream_t s) {
     case 8: return launch_spec_stream<8>(a, s);
     case 10: return launch_spec_stream<10>(a, s);
     case 11: return launch_spec_stream<11>(a, s);
-    case 12: return launch_spec_stream<12>(a, s);
+    case 12: return DSP_SPEC_WAVE ? launch_spec_wave12(a, s) : launch_spec_stream<12>(a, s);
     case 14: return launch_spec_stream<14>(a, s);
     default: break;
   }

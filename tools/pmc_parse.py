@@ -23,7 +23,7 @@ def short(name):
         return "chain_prep"
     if "k_src" in name:
         return "src_poly"
-    if "k_spec_real" in name or "k_spec_stream" in name:
+    if "k_spec_real" in name or "k_spec_stream" in name or "k_spec_wave" in name:
         return "spectrum"
     m = re.search(r"k_iir_wave<(\d+), (\d+)", name)
     if m:
