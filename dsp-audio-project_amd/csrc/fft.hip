@@ -644,15 +644,17 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
 }
 
 // Resident workgroups per CU for a kernel (asked once per calling thread and
-// kernel instance; thread_local: no state shared between threads).
-template <class Kern>
-int resident_groups(Kern k, int threads, size_t shm) {
+// kernel instance; thread_local: no state shared between threads).  The
+// kernel is a template argument so that every kernel has its own cache (as a
+// function argument, every instance of one signature shared it).
+template <auto K>
+int resident_groups(int threads, size_t shm) {
   thread_local int dev = -1, cached = 0;
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) return 0;
   if (d != dev || cached <= 0) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K),
                                                      threads, shm) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
       return 0;
@@ -669,7 +671,7 @@ int launch_spec_stream(const FftArgs& a, hipStream_t s) {
   const size_t shm = (size_t)TPBX * PL::PADN * sizeof(float2);
   if (int rc = allow_lds(k_spec_stream<LOG2N, TPBX>, shm)) return rc;
   const int64_t units = ceil_div(a.B, TPBX);
-  const int res = resident_groups(k_spec_stream<LOG2N, TPBX>, TPBX * PL::TPT, shm);
+  const int res = resident_groups<k_spec_stream<LOG2N, TPBX>>(TPBX * PL::TPT, shm);
   DSP_REQUIRE(res > 0, "occupancy query failed");
   const unsigned grid = (unsigned)(units < res ? units : res);
   hipLaunchKernelGGL((k_spec_stream<LOG2N, TPBX>), dim3(grid), dim3(TPBX * PL::TPT), shm, s, a,
@@ -709,10 +711,10 @@ __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t
 }
 
 #ifndef DSP_SPEC_WAVE
-#define DSP_SPEC_WAVE 0
+#define DSP_SPEC_WAVE 1
 #endif
-#ifndef DSP_SPEC_WAVE_OCC
-#define DSP_SPEC_WAVE_OCC 2  // waves per SIMD k_spec_wave12 is compiled for
+#ifndef DSP_SPEC_WAVE_PF_MIN
+#define DSP_SPEC_WAVE_PF_MIN 8  // transforms per resident wave from which the prefetching build runs
 #endif
 constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
 constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
@@ -824,8 +826,12 @@ __device__ __forceinline__ void wave_frame_load(const FftArgs& a, int64_t t, int
     raw[n1] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * lane, 512 * n1, 2);
 }
 
+// PF = 1: the next frame's samples load into 64 more VGPRs while this one
+// computes (226 VGPRs, 2 waves per SIMD); PF = 0: no prefetch, 149 VGPRs and 3
+// waves per SIMD.  Same arithmetic, same bits.
+template <int PF>
 __global__ __launch_bounds__(64 * kWavePerGroup)
-__attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVE_OCC))) void k_spec_wave12(FftArgs a) {
+__attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
   constexpr int N = 4096, NH = 2048;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   const int lane = threadIdx.x & 63;
@@ -842,21 +848,13 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVE_OCC))) void k_spec_wave12(FftAr
   const int src = ((1 - lane) & 63) << 2;   // bpermute address of Z[-K]'s lane
   const int K0 = k1 + 1024 * hi;
   const float sg = hi ? -1.f : 1.f;
-  const pf2* twp = reinterpret_cast<const pf2*>(a.tw);
-  const pf2 wl = twp[2 * lane];             // W_2048^lane
-  const pf2 wb = twp[K0];                   // W_4096^K0
-  pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
-#pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    const int m = (16 * lane * k) & (N - 1);
-    w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
-  }
   const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
   int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv;
   // the frame in flight: transform t + nw's samples load while t computes
   u32x2_t raw[32];
-  if (t < a.B) wave_frame_load(a, t, lane, raw);
+  if (PF && t < a.B) wave_frame_load(a, t, lane, raw);
   for (; t < a.B; t += nw) {
+    if (!PF) wave_frame_load(a, t, lane, raw);
     // an opaque per-iteration copy of the lane's parity: the combine's 31
     // per-lane twiddles below are loop-invariant, and hoisting them would
     // hold 62 VGPRs
@@ -867,12 +865,25 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVE_OCC))) void k_spec_wave12(FftAr
     int z0 = 0;
     asm volatile("" : "+s"(z0));
     const pf2* win = wl0 + z0;
-    pf2 v[32];
+    const pf2* twp = reinterpret_cast<const pf2*>(a.tw) + z0;
+    const pf2 wl = twp[2 * lane];             // W_2048^lane
+    const pf2 wb = twp[K0];                   // W_4096^K0
+    pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
 #pragma unroll
-    for (int n1 = 0; n1 < 32; ++n1)
+    for (int k = 1; k < 4; ++k) {
+      const int m = (16 * lane * k) & (N - 1);
+      w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
+    }
+    pf2 v[32];
+    // (the window's LDS reads in groups of 8: all 32 in flight would hold 64
+    // VGPRs beside the samples)
+#pragma unroll
+    for (int n1 = 0; n1 < 32; ++n1) {
+      if (n1 % 8 == 0) asm volatile("" ::: "memory");
       v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} *
               win[64 * n1 + lane];
-    if (t + nw < a.B) wave_frame_load(a, t + nw, lane, raw);
+    }
+    if (PF && t + nw < a.B) wave_frame_load(a, t + nw, lane, raw);
     // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
     // powers come from the table every 8 steps and by products in between)
     pdft32(v);
@@ -932,16 +943,30 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVE_OCC))) void k_spec_wave12(FftAr
   }
 }
 
-int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
-  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
-  if (int rc = allow_lds(k_spec_wave12, shm)) return rc;
+template <int PF>
+int launch_spec_wave12_pf(const FftArgs& a, hipStream_t s, size_t shm, int res) {
   const int64_t groups = ceil_div(a.B, kWavePerGroup);
-  const int res = resident_groups(k_spec_wave12, 64 * kWavePerGroup, shm);
-  DSP_REQUIRE(res > 0, "occupancy query failed");
   const unsigned grid = (unsigned)(groups < res ? groups : res);
-  hipLaunchKernelGGL(k_spec_wave12, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
+  hipLaunchKernelGGL(k_spec_wave12<PF>, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
   DSP_LAUNCHED("k_spec_wave12");
   return DSP_OK;
+}
+
+// The prefetching build when every resident wave gets >= DSP_SPEC_WAVE_PF_MIN
+// transforms (its first frame's load is not hidden, and it holds a third
+// fewer waves): config 4's 32768 transforms (16 per wave) 0.197 vs 0.204 ms,
+// config 5's 8192 (4 per wave) 0.058 vs 0.054 ms (profiles/r03_spec_wave_pf_ab.jsonl).
+int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
+  if (int rc = allow_lds(k_spec_wave12<0>, shm)) return rc;
+  if (int rc = allow_lds(k_spec_wave12<1>, shm)) return rc;
+  const int res1 = resident_groups<k_spec_wave12<1>>(64 * kWavePerGroup, shm);
+  DSP_REQUIRE(res1 > 0, "occupancy query failed");
+  if (a.B >= (int64_t)DSP_SPEC_WAVE_PF_MIN * kWavePerGroup * res1)
+    return launch_spec_wave12_pf<1>(a, s, shm, res1);
+  const int res0 = resident_groups<k_spec_wave12<0>>(64 * kWavePerGroup, shm);
+  DSP_REQUIRE(res0 > 0, "occupancy query failed");
+  return launch_spec_wave12_pf<0>(a, s, shm, res0);
 }
 
 // ---------------------------------------------------------------------------

@@ -319,6 +319,27 @@ def test_spectrum_matches_reference(gpu):
                 dc.calcular_espectro_magnitud(np.ones(int(n)), 44100)
 
 
+def test_spectrum_4096_large_batch_bitwise_small_batch(gpu):
+    """The 4096-point spectrum kernel (k_spec_wave12) prefetches the next
+    frame when every resident wave gets >= 8 transforms (>= 16384 on MI355X)
+    and not below: the large batch's rows are bitwise the same rows computed
+    in a small batch, and within FFT_RTOL of float64 numpy (Hann of
+    dsp_core.py:87, |rfft|) -- on an unaligned segment start."""
+    B, n, start = 20000, 4196, 37
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.rand((B, n), device=gpu, generator=g) * 2 - 1
+    big = _ops().spectrum(x, start, 4096, 4096)
+    rows = [0, 1, 4999, 12345, B - 1]
+    small = _ops().spectrum(x[rows].contiguous(), start, 4096, 4096)
+    assert torch.equal(big[rows], small)
+    k = np.arange(4096)
+    w = 0.5 - 0.5 * np.cos(2 * np.pi * k / 4095)
+    seg = x[rows, start:start + 4096].double().cpu().numpy()
+    ref = np.abs(np.fft.rfft(seg * w, axis=1))
+    got = small.cpu().numpy()
+    assert np.max(np.abs(got - ref), axis=1).max() <= FFT_RTOL * ref.max()
+
+
 def test_stft_frames_match_reference_recipe(gpu):
     """Every frame of the spectrogram extension equals the reference's spectrum
     recipe (Hann, radix-2 FFT, |X|) on that frame: max|d| <= 1e-5 * max|X|
