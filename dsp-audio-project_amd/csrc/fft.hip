@@ -698,10 +698,10 @@ int launch_spec_stream(const FftArgs& a, hipStream_t s) {
 // lanes 0 and 1, each other's partners at register 32 - j, take the previous
 // bpermute's value (and their own Z at j = 0).  For fixed j, |X[K]| is two runs
 // of 32 consecutive floats across the wave.  Per transform and lane: 32 sample
-// + 32 window + 32 twiddle loads, 128 LDS accesses, 64 bpermutes, 64 DPP moves,
-// 32 stores, no barrier: k_spec_stream's three LDS Stockham passes need a
-// workgroup barrier each and more instructions, and that kernel is
-// issue-bound.
+// loads (b64) and 5 twiddle loads, 32 window reads from the workgroup's LDS
+// copy, 128 transpose accesses, 64 bpermutes, 64 DPP moves, 32 stores, no
+// barrier: 35 % fewer VALU instructions than k_spec_stream's three LDS
+// Stockham passes (which need a workgroup barrier each), DESIGN.md section 3.3.
 // ---------------------------------------------------------------------------
 // W_N^m for any m from the table exp(-2 pi i k / N), k < N/2.
 __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t m, int64_t N) {
