@@ -861,7 +861,8 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
     float hf = (float)hi;
     asm volatile("" : "+v"(hf));
     const pf2 hh = pf2{hf, hf};
-    // (and of the window's address: its 32 LDS reads would be hoisted too)
+    // (and of the window and twiddle addresses: hoisted, the window's 32 LDS
+    // reads hold 64 VGPRs and the twiddles ~20)
     int z0 = 0;
     asm volatile("" : "+s"(z0));
     const pf2* win = wl0 + z0;
