@@ -713,15 +713,19 @@ __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t
 #ifndef DSP_SPEC_WAVE
 #define DSP_SPEC_WAVE 1
 #endif
-#ifndef DSP_SPEC_WAVE_PF_MIN
-#define DSP_SPEC_WAVE_PF_MIN 8  // transforms per resident wave from which the prefetching build runs
+#ifndef DSP_SPEC_WAVE_PF
+#define DSP_SPEC_WAVE_PF 0  // 1: prefetch the next frame in 64 VGPRs (2 waves per SIMD)
 #endif
 constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
 constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
 constexpr int kWavePerGroup = 4;
 
-// W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).
-__device__ __forceinline__ pf2 w128(int j) {
+// W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).  oz: an
+// opaque zero OR-ed into the bits, so that the constants are formed where they
+// are used (SALU) instead of hoisted out of the caller's loop: hoisted, the
+// wave kernel's ~100 constant SGPRs spilled through v_writelane/v_readlane,
+// ~160 VALU instructions per transform.
+__device__ __forceinline__ pf2 w128(int j, int oz = 0) {
   constexpr float c[33] = {
       1.000000000e+00f, 9.987954562e-01f, 9.951847267e-01f, 9.891765100e-01f,
       9.807852804e-01f, 9.700312532e-01f, 9.569403357e-01f, 9.415440652e-01f,
@@ -736,17 +740,18 @@ __device__ __forceinline__ pf2 w128(int j) {
   j &= 63;
   const float cs = j <= 32 ? c[j] : -c[64 - j];
   const float sn = j <= 32 ? c[32 - j] : c[j - 32];
-  return pf2{sgn * cs, -sgn * sn};
+  return pf2{__int_as_float(__float_as_int(sgn * cs) | oz),
+             __int_as_float(__float_as_int(-sgn * sn) | oz)};
 }
 
 // a * W_128^j for a compile-time j; exact for multiples of 32.
-__device__ __forceinline__ pf2 pw128(pf2 a, int j) {
+__device__ __forceinline__ pf2 pw128(pf2 a, int j, int oz = 0) {
   j &= 127;
   if (j == 0) return a;
   if (j == 32) return pmi(a);
   if (j == 64) return -a;
   if (j == 96) return -pmi(a);
-  return pcmul(a, w128(j));
+  return pcmul(a, w128(j, oz));
 }
 
 __device__ __forceinline__ void pdft4(pf2& a0, pf2& a1, pf2& a2, pf2& a3) {
@@ -759,13 +764,13 @@ __device__ __forceinline__ void pdft4(pf2& a0, pf2& a1, pf2& a2, pf2& a3) {
 
 // In-place 16- and 32-point DFTs, natural order in and out (dft<16>'s 4 x 4
 // split; 32 = 2 x 16 with a radix-2 combine).
-__device__ __forceinline__ void pdft16(pf2 (&v)[16]) {
+__device__ __forceinline__ void pdft16(pf2 (&v)[16], int oz = 0) {
 #pragma unroll
   for (int n2 = 0; n2 < 4; ++n2) pdft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
 #pragma unroll
   for (int k1 = 1; k1 < 4; ++k1)
 #pragma unroll
-    for (int n2 = 1; n2 < 4; ++n2) v[4 * k1 + n2] = pw128(v[4 * k1 + n2], 8 * n2 * k1);
+    for (int n2 = 1; n2 < 4; ++n2) v[4 * k1 + n2] = pw128(v[4 * k1 + n2], 8 * n2 * k1, oz);
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) pdft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
   pf2 o[16];
@@ -777,18 +782,18 @@ __device__ __forceinline__ void pdft16(pf2 (&v)[16]) {
   for (int i = 0; i < 16; ++i) v[i] = o[i];
 }
 
-__device__ __forceinline__ void pdft32(pf2 (&v)[32]) {
+__device__ __forceinline__ void pdft32(pf2 (&v)[32], int oz = 0) {
   pf2 e[16], o[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     e[i] = v[2 * i];
     o[i] = v[2 * i + 1];
   }
-  pdft16(e);
-  pdft16(o);
+  pdft16(e, oz);
+  pdft16(o, oz);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const pf2 t = pw128(o[k], 4 * k);
+    const pf2 t = pw128(o[k], 4 * k, oz);
     v[k] = e[k] + t;
     v[k + 16] = e[k] - t;
   }
@@ -887,7 +892,7 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
     if (PF && t + nw < a.B) wave_frame_load(a, t + nw, lane, raw);
     // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
     // powers come from the table every 8 steps and by products in between)
-    pdft32(v);
+    pdft32(v, z0);
     {
       pf2 p = 0.5f * wl;
       v[0] *= 0.5f;
@@ -916,13 +921,13 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
     for (int m = 0; m < 32; ++m) v[m].y = buf[rd + 2 * m];
     // B: DFT over m, then the radix-2 step across the lane pair: lane h = 1
     // scales its F_1 by W_64^j, the pair swaps, and Z = own * (+-1) + other
-    pdft32(v);
+    pdft32(v, z0);
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       pf2 u = v[j];
       if (j > 0) {
         const pf2 one = pf2{1.f, 0.f};
-        u = vcmul(u, one + hh * (w128(2 * j) - one));  // h ? W_64^j : 1
+        u = vcmul(u, one + hh * (w128(2 * j, z0) - one));  // h ? W_64^j : 1
       }
       v[j] = u * sg + pf2{swap_pair(u.x), swap_pair(u.y)};
     }
@@ -937,7 +942,7 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
       const pf2 zk = v[j];
       const pf2 sm = pf2{zk.x + zm.x, zk.y - zm.y};
       const pf2 d = pf2{zk.x - zm.x, zk.y + zm.y};
-      const pf2 x = vcfma(d, pw128(wb, j + 32), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
+      const pf2 x = vcfma(d, pw128(wb, j + 32, z0), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
       mr[K0 + 32 * j] = cabsf_(make_float2(x.x, x.y));
     }
     if (lane == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
@@ -953,21 +958,17 @@ int launch_spec_wave12_pf(const FftArgs& a, hipStream_t s, size_t shm, int res) 
   return DSP_OK;
 }
 
-// The prefetching build when every resident wave gets >= DSP_SPEC_WAVE_PF_MIN
-// transforms (its first frame's load is not hidden, and it holds a third
-// fewer waves): config 4's 32768 transforms (16 per wave) 0.197 vs 0.204 ms,
-// config 5's 8192 (4 per wave) 0.058 vs 0.054 ms (profiles/r03_spec_wave_pf_ab.jsonl).
+// PF = 0 since the opaque-zero constants (w128) cut its VALU by 12 %: 0.194 vs
+// 0.199 ms (PF = 1) at config 4, 0.052 vs 0.056 at config 5
+// (profiles/r03_spec_wave_oz_ab.jsonl); with the hoisted constants PF = 1 had
+// won at config 4 (profiles/r03_spec_wave_pf_ab.jsonl).
 int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+  constexpr int PF = DSP_SPEC_WAVE_PF;
   const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
-  if (int rc = allow_lds(k_spec_wave12<0>, shm)) return rc;
-  if (int rc = allow_lds(k_spec_wave12<1>, shm)) return rc;
-  const int res1 = resident_groups<k_spec_wave12<1>>(64 * kWavePerGroup, shm);
-  DSP_REQUIRE(res1 > 0, "occupancy query failed");
-  if (a.B >= (int64_t)DSP_SPEC_WAVE_PF_MIN * kWavePerGroup * res1)
-    return launch_spec_wave12_pf<1>(a, s, shm, res1);
-  const int res0 = resident_groups<k_spec_wave12<0>>(64 * kWavePerGroup, shm);
-  DSP_REQUIRE(res0 > 0, "occupancy query failed");
-  return launch_spec_wave12_pf<0>(a, s, shm, res0);
+  if (int rc = allow_lds(k_spec_wave12<PF>, shm)) return rc;
+  const int res = resident_groups<k_spec_wave12<PF>>(64 * kWavePerGroup, shm);
+  DSP_REQUIRE(res > 0, "occupancy query failed");
+  return launch_spec_wave12_pf<PF>(a, s, shm, res);
 }
 
 // ---------------------------------------------------------------------------

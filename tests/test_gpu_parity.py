@@ -320,11 +320,11 @@ def test_spectrum_matches_reference(gpu):
 
 
 def test_spectrum_4096_large_batch_bitwise_small_batch(gpu):
-    """The 4096-point spectrum kernel (k_spec_wave12) prefetches the next
-    frame when every resident wave gets >= 8 transforms (>= 16384 on MI355X)
-    and not below: the large batch's rows are bitwise the same rows computed
-    in a small batch, and within FFT_RTOL of float64 numpy (Hann of
-    dsp_core.py:87, |rfft|) -- on an unaligned segment start."""
+    """The 4096-point spectrum kernel (k_spec_wave12, a persistent grid of
+    one transform per wave at a time) over a batch ~10x its resident waves:
+    the large batch's rows are bitwise the same rows computed in a small
+    batch, and within FFT_RTOL of float64 numpy (Hann of dsp_core.py:87,
+    |rfft|) -- on an unaligned segment start."""
     B, n, start = 20000, 4196, 37
     g = torch.Generator(device=gpu).manual_seed(5)
     x = torch.rand((B, n), device=gpu, generator=g) * 2 - 1

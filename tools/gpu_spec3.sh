@@ -16,4 +16,4 @@ for l in open("gpurun_out/spec3/timing.log"):
         d = json.loads(l)
         print(d["tag"], d["B"], d["step_ms"], d["kernels_ms"])
 PY
-python tools/tile_ab.py --compare c3_libdspcore_stream c3_libdspcore | tee $OUT/compare.txt
+python tools/tile_ab.py --compare c3_libdspcore_prev c3_libdspcore | tee $OUT/compare.txt
