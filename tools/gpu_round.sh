@@ -1,6 +1,6 @@
 # Round measurement: GPU parity tests, smoke, bench lines (config 4 default and
 # config 5), rocprofv3 kernel stats of the same bench commands, PMC passes
-# (HBM traffic + SQ counters) for both -> gpurun_out/$TAG/.
+# (HBM traffic + SQ counters, run first so the bench lines cite them) -> gpurun_out/$TAG/.
 #   bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-round}
@@ -13,6 +13,16 @@ rc=$?; tail -2 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
 tail -1 "$OUT/smoke.log"
+# PMC passes first, so that the bench lines below cite this run's traffic:
+# pmc_traffic.json is rewritten on the box (and copied back under gpurun_out/).
+cd "$GRAFT_REPO_ROOT"
+for c in c4 c5 c3; do
+  case $c in c4) wl=config4; ch=32768;; c5) wl=config5; ch=8192;; c3) wl=config3; ch=4096;; esac
+  bash tools/pmc_chain.sh "$TAG/pmc_$c" 3 $c > "$OUT/pmc_$c.log" 2>&1 || { tail -20 "$OUT/pmc_$c.log"; exit 1; }
+  python tools/pmc_parse.py "$OUT/pmc_$c/pmc" --write $wl $ch "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/kernels_once.py (profiles/${TAG}_${c}_pmc_summary.txt)" > /dev/null || exit 1
+  grep -E "^==|traffic" "$OUT/pmc_$c/pmc_summary.txt"
+done
+cp pmc_traffic.json "$OUT/pmc_traffic.json"
 for c in c4 c5; do
   echo "== bench $c"
   extra=""; [ $c = c5 ] && extra="--no-extras"
@@ -27,9 +37,4 @@ for c in c4 c5; do
   cut -d, -f1-4 "$OUT/kernel_stats_$c.csv" | head -4 | cut -c1-200
   grep '^{' "$OUT/prof_$c.log" | cut -c1-200
 done
-cd "$GRAFT_REPO_ROOT"
-bash tools/pmc_chain.sh "$TAG/pmc_c4" 3 c4 > "$OUT/pmc_c4.log" 2>&1 || { tail -20 "$OUT/pmc_c4.log"; exit 1; }
-bash tools/pmc_chain.sh "$TAG/pmc_c5" 3 c5 > "$OUT/pmc_c5.log" 2>&1 || { tail -20 "$OUT/pmc_c5.log"; exit 1; }
-bash tools/pmc_chain.sh "$TAG/pmc_c3" 3 c3 > "$OUT/pmc_c3.log" 2>&1 || { tail -20 "$OUT/pmc_c3.log"; exit 1; }
-grep -E "^==|traffic" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c4/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c5/pmc_summary.txt" "$GRAFT_REPO_ROOT/gpurun_out/$TAG/pmc_c3/pmc_summary.txt"
 echo done
