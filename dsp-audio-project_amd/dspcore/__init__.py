@@ -7,16 +7,17 @@ Layers (bottom-up):
   ops             per-kernel device operators on torch CUDA tensors
   chain           batched SRC -> EQ -> spectrum plan (the benchmarked path)
   shard           one host thread per GPU over contiguous channel ranges
+  host            numpy batches through the chain with PCIe copies overlapped
 The reference-compatible drop-in is dsp-audio-project_amd/modules/dsp_core.py.
 """
 from . import design  # noqa: F401
 
-__all__ = ["design", "ops", "chain", "shard"]
+__all__ = ["design", "ops", "chain", "shard", "host"]
 __version__ = "1.3.0"
 
 
 def __getattr__(name):  # lazy: importing design must not require the GPU library
-    if name in ("ops", "chain", "shard", "_lib"):
+    if name in ("ops", "chain", "shard", "host", "_lib"):
         import importlib
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

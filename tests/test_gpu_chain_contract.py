@@ -298,3 +298,41 @@ def test_chain_app_rerun_spectra_x_y_z(gpu):
         Chain(cfg, 2, gpu, spectra=("x",))
     with pytest.raises(ValueError):
         Chain(cfg, 2, gpu, keep_y=False, spectra=("y", "z"))
+
+
+def test_host_chain_pipelined_numpy_matches_chain_run(gpu):
+    """dspcore.host.HostChain (numpy in/out, channel blocks through a ring of
+    slots with pinned staging and overlapped copies): 300 channels in blocks of
+    64 (a short, zero-padded last block) are bitwise Chain.run's rows on the
+    whole batch -- the single-pass kernel's rows do not depend on the batch --
+    and spot rows match the oracle; keep_y=False returns y = None with z and
+    |Z| unchanged; a second call reuses the pinned outputs."""
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.host import HostChain
+    from oracle import dsp_ref_cpu as orc
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-1, 1, (300, 4800)).astype(np.float32)
+    cfg = ChainConfig(4800, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=2048)
+    hc = HostChain(cfg, gpu, block=64, slots=3)
+    y, z, mag = hc.run(x, copy=True)
+    ch = Chain(cfg, 300, gpu)
+    ry, rz, rmag = (t.cpu().numpy() for t in ch.run(torch.from_numpy(x).to(gpu)))
+    assert ch.tile_len > 0
+    np.testing.assert_array_equal(y, ry)
+    np.testing.assert_array_equal(z, rz)
+    np.testing.assert_array_equal(mag, rmag)
+    for b in (0, 299):
+        oy, oz, _, om, _ = orc.chain(x[b], 48000, 3, 2, orc.CONFIG3_GAINS, None, 2048)
+        assert np.max(np.abs(y[b] - oy)) <= SRC_ATOL
+        assert np.max(np.abs(z[b] - oz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - om)) <= CHAIN_MAG_RTOL * np.max(om)
+    y2, z2, mag2 = hc.run(x[::-1])
+    np.testing.assert_array_equal(z2, rz[::-1])
+    np.testing.assert_array_equal(mag2, rmag[::-1])
+    hn = HostChain(cfg, gpu, block=128, slots=2, keep_y=False)
+    yn, zn, mn = hn.run(x)
+    assert yn is None
+    np.testing.assert_array_equal(zn, rz)
+    np.testing.assert_array_equal(mn, rmag)
+    with pytest.raises(ValueError):
+        hc.run(x[:, :100])
