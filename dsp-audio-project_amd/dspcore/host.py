@@ -16,8 +16,8 @@ pinned input staging buffer and HIP stream:
     D2H of y, z, |Z| of block i-1 into pinned output  (other copy engine)
 
 so the host copy, both PCIe directions and the kernels overlap.  The outputs
-are numpy views of pinned host buffers the object owns and reuses: they stay
-valid until the next `run` with a different batch size, or pass `copy=True`.
+are numpy views of pinned host buffers the object owns and reuses: the next
+`run` overwrites them (pass `copy=True` to keep a call's results).
 
 Each block is a full `Chain` call of `block` channels (a short last block is
 zero-padded); the rows equal `Chain(cfg, block).run` bitwise, and on the
