@@ -718,7 +718,13 @@ __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t
 #endif
 constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
 constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
-constexpr int kWavePerGroup = 4;
+#ifndef DSP_SPEC_WPG
+#define DSP_SPEC_WPG 4
+#endif
+#ifndef DSP_SPEC_WPE
+#define DSP_SPEC_WPE 3
+#endif
+constexpr int kWavePerGroup = DSP_SPEC_WPG;
 
 // W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).  oz: an
 // opaque zero OR-ed into the bits, so that the constants are formed where they
@@ -836,7 +842,7 @@ __device__ __forceinline__ void wave_frame_load(const FftArgs& a, int64_t t, int
 // waves per SIMD.  Same arithmetic, same bits.
 template <int PF>
 __global__ __launch_bounds__(64 * kWavePerGroup)
-__attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void k_spec_wave12(FftArgs a) {
+__attribute__((amdgpu_waves_per_eu(PF ? 2 : DSP_SPEC_WPE))) void k_spec_wave12(FftArgs a) {
   constexpr int N = 4096, NH = 2048;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   const int lane = threadIdx.x & 63;
