@@ -133,7 +133,11 @@ def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
     measured 0.86 -> 1.19 -> 0.89 ms over its first 20 launches), then W untimed
     warmup steps, then K steps bracketed by barrier + sync on both sides.
     Returns the elapsed seconds, maxed over ranks when `dist` is initialised
-    (a gloo group: the max is a CPU all-reduce)."""
+    (a gloo group: the max is a CPU all-reduce).  Each rank's clock runs from
+    the start barrier to its own final sync: the end barrier still holds every
+    rank until the slowest is done, but its gloo round trips (a sizeable share
+    of a ~17 ms N = 8 timed region) stay out of the time; the max over ranks is
+    the job's time."""
     t_pre = time.perf_counter()
     while preheat_s > 0:
         step()
@@ -150,9 +154,9 @@ def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
     for _ in range(steps):
         step()
     sync()
+    elapsed = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
