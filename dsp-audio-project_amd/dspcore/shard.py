@@ -65,3 +65,43 @@ def run_sharded(fn, x: np.ndarray, devices: list | None = None) -> list:
     if errors:
         raise errors[0]
     return [np.concatenate([r[k] for r in results], axis=0) for k in range(len(results[0]))]
+
+
+def run_sharded_host(cfg, x: np.ndarray, devices: list | None = None, block: int = 64,
+                     slots: int = 4) -> tuple:
+    """y, z, |Z| of a host-resident [B, n_in] batch over several devices: one
+    dspcore.host.HostChain per device on its contiguous channel range, each
+    driven from its own host thread (pinned staging, overlapped copies), the
+    rows gathered into fresh numpy arrays.  Rows are bitwise those of one
+    HostChain on the whole batch (the chain is planned per block, the same
+    on every device)."""
+    from .host import HostChain
+    if devices is None:
+        devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    x = np.asarray(x, dtype=np.float32)
+    ranges = shard_ranges(x.shape[0], len(devices))
+    runners = [HostChain(cfg, devices[i], block=block, slots=slots) for i in range(len(ranges))]
+    n_out, n_mag = runners[0].n_out, runners[0].n_mag
+    B = x.shape[0]
+    y = np.empty((B, n_out), np.float32)
+    z = np.empty((B, n_out), np.float32)
+    mag = np.empty((B, n_mag), np.float32)
+    errors: list = []
+
+    def worker(i, lo, hi):
+        try:
+            with torch.cuda.device(runners[i].device):
+                oy, oz, om = runners[i].run(x[lo:hi])
+            y[lo:hi], z[lo:hi], mag[lo:hi] = oy, oz, om
+        except BaseException as e:  # re-raised on the caller's thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(i, lo, hi))
+               for i, (lo, hi) in enumerate(ranges)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return y, z, mag

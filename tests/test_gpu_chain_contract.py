@@ -336,3 +336,21 @@ def test_host_chain_pipelined_numpy_matches_chain_run(gpu):
     np.testing.assert_array_equal(mn, rmag)
     with pytest.raises(ValueError):
         hc.run(x[:, :100])
+
+
+def test_run_sharded_host_bitwise(gpu):
+    """shard.run_sharded_host: a numpy batch over 1, 2 and 3 "devices" (all
+    cuda:0 here: the 1-GPU rehearsal of one HostChain and host thread per GPU)
+    gives the same bits for every shard count."""
+    from dspcore.chain import ChainConfig
+    from dspcore.shard import run_sharded_host
+    from oracle import dsp_ref_cpu as orc
+    x = np.random.default_rng(12).uniform(-1, 1, (150, 4800)).astype(np.float32)
+    cfg = ChainConfig(4800, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=2048)
+    base = run_sharded_host(cfg, x, [gpu], block=32, slots=2)
+    for parts in (2, 3):
+        got = run_sharded_host(cfg, x, [gpu] * parts, block=32, slots=2)
+        for a, b in zip(base, got):
+            np.testing.assert_array_equal(a, b)
+    oy, oz, _, om, _ = orc.chain(x[77], 48000, 3, 2, orc.CONFIG3_GAINS, None, 2048)
+    assert np.max(np.abs(base[1][77] - oz)) <= EQ_ATOL
