@@ -77,6 +77,7 @@
 // Rows are bitwise independent of the batch size: the geometry depends on
 // (L, M, K) only.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "cascade.h"
@@ -280,7 +281,18 @@ typedef __attribute__((address_space(4))) const TileTables* tt_ptr;
 // sums of its even- and odd-indexed x samples in the halves of one register
 // pair, pairs p ascending, and y = even + odd -- the summation order of
 // k_src_reg's packed path (src_poly.hip), so y is bitwise the SRC kernel's.
-template <class GEO, int H0, int NH>
+// DLY: branch 0's taps are zero but for its centre tap u = TT / 2 (the
+// host's kernel taps with the sinc-zero noise flushed, design.kernel_taps;
+// dsp_chain_tile_tables checks it and marks the key): its outputs, every L-th,
+// are that tap times one sample -- one multiply instead of NP packed FMAs, and
+// bitwise what the FMA chain gives on these taps (t x rounded once; the zero
+// taps add signed zeros).  Outputs of other branches are unchanged.
+template <class GEO>
+constexpr bool dly_out(int i) { return GEO::phi(i) == 0; }
+template <class GEO>
+constexpr int dly_slot() { return GEO::TT / 2 + (branch_parity<GEO>(0) > 0 ? 1 : 0); }
+
+template <class GEO, int H0, int NH, bool DLY = false>
 __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[GEO::TSUB]) {
   constexpr int V0 = GEO::qs(H0) / 4 * 4;
   constexpr int V1 = GEO::qs(H0 + NH - 1) + 2 * GEO::NP;
@@ -306,11 +318,25 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
     for (int ph = 0; ph < GEO::L; ++ph) t[ph] = f32x2{tq->TP[p][ph][0], tq->TP[p][ph][1]};
 #pragma unroll
     for (int i = 0; i < NH; ++i)
-      acc[i] = __builtin_elementwise_fma(t[GEO::phi(H0 + i)],
-                                         w[(GEO::qs(H0 + i) - V0) / 2 + p], acc[i]);
+      if (!(DLY && dly_out<GEO>(H0 + i)))
+        acc[i] = __builtin_elementwise_fma(t[GEO::phi(H0 + i)],
+                                           w[(GEO::qs(H0 + i) - V0) / 2 + p], acc[i]);
+  }
+  float td = 0.f;
+  if (DLY) {
+    tt_ptr tq = tt;
+    asm volatile("" : "+s"(tq));
+    td = tq->TP[dly_slot<GEO>() / 2][0][dly_slot<GEO>() % 2];
   }
 #pragma unroll
-  for (int i = 0; i < NH; ++i) y[H0 + i] = acc[i].x + acc[i].y;
+  for (int i = 0; i < NH; ++i) {
+    if (DLY && dly_out<GEO>(H0 + i)) {
+      const f32x2 xv = w[(GEO::qs(H0 + i) - V0) / 2 + dly_slot<GEO>() / 2];
+      y[H0 + i] = td * (dly_slot<GEO>() % 2 ? xv.y : xv.x);
+    } else {
+      y[H0 + i] = acc[i].x + acc[i].y;
+    }
+  }
 }
 
 // Stores the tile's 64 x TS outputs (lane l holds outputs l*TS + i) as
@@ -746,7 +772,7 @@ constexpr int kMfWin = 32 * 63 + 16 + 64;       // window samples the B operands
 constexpr int kMfPlane = (kMfWin / 8 + 15) / 16 * 16 * 8;  // halfs per plane (whole swizzle groups)
 __device__ __forceinline__ int mf_chunk(int c) { return c ^ ((c >> 4) & 3); }
 
-template <class GEO>
+template <class GEO, bool DLY = false>  // (DLY: the VALU SRC's shortcut; unused here)
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
   constexpr int TS = GEO::TSUB;
@@ -879,7 +905,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   }
 }
 #else
-template <class GEO>
+template <class GEO, bool DLY = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
   constexpr int TS = GEO::TSUB;
@@ -913,13 +939,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   {
     const float* xw = lds + 36 * lane;
     static_assert(TS == 48, "four parts");
-    src_part<GEO, 0, 12>(xw, mt, y);
+    src_part<GEO, 0, 12, DLY>(xw, mt, y);
     pin(y);
-    src_part<GEO, 12, 12>(xw, mt, y);
+    src_part<GEO, 12, 12, DLY>(xw, mt, y);
     pin(y);
-    src_part<GEO, 24, 12>(xw, mt, y);
+    src_part<GEO, 24, 12, DLY>(xw, mt, y);
     pin(y);
-    src_part<GEO, 36, 12>(xw, mt, y);
+    src_part<GEO, 36, 12, DLY>(xw, mt, y);
     pin(y);
   }
   tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
@@ -1902,6 +1928,30 @@ void ct_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables*
   }
 }
 
+// Branch 0 of the L3/M2 tile a pure delay (src_part's DLY): its tap pairs are
+// zero except the centre tap's slot, which is finite and non-zero.
+#ifndef DSP_NO_DLY
+#define DSP_NO_DLY 0  // 1: never take the DLY kernel (A/B builds)
+#endif
+template <class GEO>
+bool delay_branch(const TileTables* tt) {
+  if (DSP_NO_DLY || branch_parity<GEO>(0) < 0) return false;
+  constexpr int sl = dly_slot<GEO>();
+  for (int p = 0; p < GEO::NP; ++p)
+    for (int e = 0; e < 2; ++e) {
+      const float v = tt->TP[p][0][e];
+      const bool centre = 2 * p + e == sl;
+      if (centre ? !(std::isfinite(v) && v != 0.f) : v != 0.f) return false;
+    }
+  return true;
+}
+
+// Key of tables whose taps take the DLY kernel (never 0, never the plain key).
+uint64_t dly_key(uint64_t base) {
+  const uint64_t k = base ^ 0x9e3779b97f4a7c15ull;
+  return k ? k : 2;
+}
+
 struct TileWs {
   size_t err_off, st_off, fl_off, total;
 };
@@ -1948,9 +1998,11 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   TileTables* tt = static_cast<TileTables*>(out);
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
+  bool dly = false;
   if (tp.kind == 1) {
     tap_pairs<Geo3241>(taps, K, tt);
     mfma_taps<Geo3241>(tt);
+    dly = delay_branch<Geo3241>(tt);
   } else gen_sequences(taps, K, L, M, c, tt);
   if (tp.kind == 3 || tp.kind == 4) ct_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
@@ -1967,7 +2019,8 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   tt->M = M;
   tt->K = K;
   tt->S = S;
-  tt->key = tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
+  tt->key = dly ? dly_key(tables_key(tp, n_in, n_out, K, L, M, c, sos, S))
+                : tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
   if (key) *key = tt->key;
   return DSP_OK;
 }
@@ -1978,8 +2031,11 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
                       uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s) {
   TilePlan tp;
   if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
-  // Tables built for another geometry or cascade: the two-launch chain.
-  if (key != tables_key(tp, n_in, n_out, K, L, M, c, sos, S)) return kNotFused;
+  // Tables built for another geometry or cascade: the two-launch chain.  The
+  // key also says whether the tables' taps make branch 0 a pure delay.
+  const uint64_t key0 = tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
+  const bool dly = key == dly_key(key0);
+  if (key != key0 && !dly) return kNotFused;
   auto aligned = [](const void* p, int64_t ld) {
     return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   };
@@ -2020,8 +2076,8 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.win = tp.win;
   if (tp.kind == 1) {
     TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL(k_chain_tile<Geo3241>, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s,
-                       a);
+    auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s, a);
   } else if (tp.kind == 4) {
     const size_t shm = g5_lds_bytes(tp.win);
     auto kern = k_chain_g5<160, 147>;

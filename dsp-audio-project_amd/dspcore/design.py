@@ -84,6 +84,30 @@ def src_plan(n_in: int, fs: int, M: int, L: int, num_taps: int | None = None) ->
     return SrcPlan(L, M, K, h, c, n_in, n_out, int(fs * L / M))
 
 
+# Kernel taps below this fraction of the largest are flushed to exactly zero.
+TAP_FLUSH_REL = 1e-12
+
+
+def kernel_taps(plan: SrcPlan) -> np.ndarray:
+    """float32 L*h as every SRC kernel takes it (ops.taps_tensor, Chain's
+    single-pass tables): the taps at the sinc's zeros -- every L-th tap from the
+    centre when wc = 1/L (upsampling, dsp_core.py:155), whose float64 values are
+    the rounding noise of sin(k pi) (|L h| ~ 1e-17 .. 1e-34 at K = 121) -- are
+    flushed to exactly 0.  Their contribution to y is below 1e-14 of the signal,
+    far inside the SRC tolerance (2e-6), and the polyphase branch that holds
+    the centre tap becomes a pure scaled delay: the single-pass kernel computes
+    its outputs (1/L of them) with one multiply instead of ceil(K/L) FMAs
+    (csrc/chain_tile.hip, DLY), bitwise what the FMA chains give on these taps.
+    The float64 design (generar_respuesta_impulso_sinc) is unchanged; plans
+    with L = 1 (downsampling, and aplicar_ecuacion_diferencias' FIR path) keep
+    every tap as float32(L h)."""
+    t = np.asarray(plan.taps, dtype=np.float64)
+    out = t.astype(np.float32)
+    if plan.L > 1 and t.size:
+        out[np.abs(t) <= TAP_FLUSH_REL * float(np.max(np.abs(t)))] = 0.0
+    return out
+
+
 def peaking_biquad(fc: float, fs: float, gain_db: float) -> tuple[np.ndarray, np.ndarray]:
     """RBJ-style peaking EQ with Q = 1 (reference dsp_core.py:179-203).
 

@@ -88,7 +88,9 @@ def ld(x: torch.Tensor) -> int:
 
 
 def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:
-    return torch.from_numpy(plan.taps.astype(np.float32)).to(device)
+    """The kernels' float32 taps (design.kernel_taps: sinc-zero noise flushed)."""
+    from .design import kernel_taps
+    return torch.from_numpy(kernel_taps(plan)).to(device)
 
 
 def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = None,

@@ -254,3 +254,61 @@ def test_lfilter_plan_any_order_matches_lfilter():
         design.lfilter_plan([1.0], [0.0, 1.0])
     with pytest.raises(RuntimeError, match="sections"):
         design.lfilter_plan([1.0], np.poly(0.5 * np.ones(34)))
+
+
+def test_kernel_taps_flush_only_sinc_zero_noise():
+    """design.kernel_taps: for upsampling plans (wc = 1/L) exactly the taps at
+    the sinc's zeros (every L-th from the centre, float64 noise of sin(k pi))
+    become 0 -- the centre branch is then a pure delay (the single-pass kernel's
+    DLY path) -- every other tap is float32(L h) bitwise; L = 1 plans keep all
+    taps; the flushed taps change y by less than 1e-14 per unit input."""
+    for L, M, K in ((3, 2, None), (2, 1, 127), (3, 2, 255), (160, 147, 1023)):
+        p = design.src_plan(48000, 48000, M, L, K)
+        kt = design.kernel_taps(p)
+        flushed = kt == 0
+        c = (p.K - 1) // 2
+        idx = np.arange(p.K)
+        # the sinc zeros of wc = 1/max(L, M) sit every max(L, M) taps from the
+        # centre; the Blackman window's end taps (~1e-34) are its zeros
+        sinc_zero = (idx - c) % max(L, M) == 0
+        win_end = (idx == 0) | (idx == p.K - 1)
+        assert np.all((sinc_zero | win_end)[flushed])
+        assert flushed.sum() >= (p.K - 1) // max(L, M) - 2
+        np.testing.assert_array_equal(kt[~flushed], p.taps[~flushed].astype(np.float32))
+        assert np.sum(np.abs(p.taps[flushed])) < 1e-14
+        assert kt[c] != 0
+    p = design.src_plan(48000, 48000, 2, 3)          # the benchmark's K = 121
+    kt = design.kernel_taps(p)
+    branch0 = kt[0::3]                               # taps ph = 0: indices 0, 3, .., 120
+    assert np.count_nonzero(branch0) == 1 and branch0[20] == kt[60]
+    fir = design.src_plan(100, 48000, 1, 1, 31)      # L = 1: nothing flushed
+    np.testing.assert_array_equal(design.kernel_taps(fir), fir.taps.astype(np.float32))
+
+
+def test_chain_tile_tables_mark_the_delay_branch():
+    """dsp_chain_tile_tables: with the kernel taps (branch 0 a pure delay) the
+    key differs from the one for the raw float32 taps, both are accepted by
+    the launcher's check (host-only: dsp_chain_tile_len / tables), and a
+    non-zero noise tap in branch 0 takes the plain key."""
+    import ctypes
+    from dspcore import _lib
+    lib = _lib.load()
+    p = design.src_plan(48000, 48000, 2, 3)
+    sos = np.ascontiguousarray(design.eq_plan(72000, {"Bass": 6.0}).sos)
+    nbytes = lib.dsp_chain_tile_tables_bytes()
+
+    def key_of(t32):
+        buf = np.zeros(nbytes, np.uint8)
+        k = ctypes.c_uint64(0)
+        rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, p.n_out, t32.ctypes.data,
+                                       p.K, 3, 2, p.c_offset, _lib.sos_pointer(sos),
+                                       sos.shape[0], ctypes.byref(k))
+        assert rc == 0
+        return k.value
+
+    kt = np.ascontiguousarray(design.kernel_taps(p))
+    raw = np.ascontiguousarray(p.taps.astype(np.float32))
+    assert np.any(raw[0::3] != 0) and key_of(kt) != key_of(raw)
+    noisy = kt.copy()
+    noisy[3] = 1e-20
+    assert key_of(noisy) == key_of(raw)
