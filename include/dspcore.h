@@ -214,6 +214,14 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * and the key to every call), 1 when it does not (the two-launch path serves
  * it; nothing to copy; *key = 0), DSP_EINVAL on bad arguments.  With
  * tile_tables == NULL dsp_chain_f32 takes the two-launch path.
+ * Delay branch (L3/M2 kernel): when the taps of polyphase branch 0 are all
+ * exactly zero but its centre tap (what dspcore.design.kernel_taps makes of
+ * the reference's wc = 1/L design: the sinc-zero noise taps, |L h| <= 1e-12
+ * max, flushed to 0), the key says so and dsp_chain_f32 computes that
+ * branch's outputs (every third) with one multiply each -- bitwise what the
+ * FMAs give on those taps.  Raw taps keep a non-zero noise tap there and take
+ * the plain kernel.  Pass the same taps to dsp_chain_f32 and to the SRC
+ * entry points so y stays bitwise equal across paths.
  *
  * Two-launch path (any other geometry, or dsp_chain_path(1)): SRC, then the
  * cascade.  With `xstate_table` (device, float64 [xstate_rows][2S], may be
