@@ -95,6 +95,9 @@ constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 // Config 5 (160/147): k_chain_gct; -DDSP_C5_G5=1 builds the class-uniform
 // k_chain_g5 instead (measured 22 % slower).
+#ifndef DSP_GCT_T7
+#define DSP_GCT_T7 1  // 0: every output reads and FMAs all 5 tap pairs (A/B builds)
+#endif
 #ifndef DSP_C5_G5
 #define DSP_C5_G5 0
 #endif
@@ -1108,7 +1111,10 @@ k_chain_gen(TileArgs a) {
 // chain; the extra slots hold zero taps (x * 0 + acc == acc, and +0 stays
 // +0), so y = even + odd is bitwise k_chain_gen's and k_src_generic's.
 // ---------------------------------------------------------------------------
-template <int L, int M>
+// T7 (T <= 7 taps per branch, config 5's K = 1023): an output whose g_i is
+// even has shift d_i in {0, 1}, so its taps fill slots 0..7 and slots 8, 9 are
+// zero: the last tap-pair read and FMA are skipped (bitwise the same y).
+template <int L, int M, bool T7 = false>
 __global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
 k_chain_gct(TileArgs a) {
   static_assert(M < L, "q advances by 0 or 1 per output");
@@ -1172,15 +1178,18 @@ k_chain_gct(TileArgs a) {
 #pragma unroll
     for (int i = 0; i < kGenTS; ++i) {
       const int g2 = (i * M / L) / 2;
+      const bool last = !(T7 && ((i * M / L) % 2 == 0));
       const f32x4 t0 = *reinterpret_cast<const f32x4*>(row + kCtRow * i);
       const f32x4 t1 = *reinterpret_cast<const f32x4*>(row + kCtRow * i + 4);
-      const f32x2 t2 = *reinterpret_cast<const f32x2*>(row + kCtRow * i + 8);
       f32x2 acc = {0.f, 0.f};
       acc = __builtin_elementwise_fma(f32x2{t0.x, t0.y}, X[g2], acc);
       acc = __builtin_elementwise_fma(f32x2{t0.z, t0.w}, X[g2 + 1], acc);
       acc = __builtin_elementwise_fma(f32x2{t1.x, t1.y}, X[g2 + 2], acc);
       acc = __builtin_elementwise_fma(f32x2{t1.z, t1.w}, X[g2 + 3], acc);
-      acc = __builtin_elementwise_fma(t2, X[g2 + 4], acc);
+      if (last) {
+        const f32x2 t2 = *reinterpret_cast<const f32x2*>(row + kCtRow * i + 8);
+        acc = __builtin_elementwise_fma(t2, X[g2 + 4], acc);
+      }
       y[i] = acc.x + acc.y;
     }
   }
@@ -2088,7 +2097,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
     const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
-    auto kern = k_chain_gct<160, 147>;
+    auto kern = (DSP_GCT_T7 && a.T <= 7) ? k_chain_gct<160, 147, true> : k_chain_gct<160, 147, false>;
     if (int rc = allow_lds(kern, shm)) return rc;
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)),
