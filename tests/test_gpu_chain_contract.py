@@ -354,3 +354,28 @@ def test_run_sharded_host_bitwise(gpu):
             np.testing.assert_array_equal(a, b)
     oy, oz, _, om, _ = orc.chain(x[77], 48000, 3, 2, orc.CONFIG3_GAINS, None, 2048)
     assert np.max(np.abs(base[1][77] - oz)) <= EQ_ATOL
+
+
+def test_single_pass_delay_branch_index_map_bit_exact(gpu):
+    """The single-pass kernel's delay-branch path (k_chain_tile<Geo3241, DLY>):
+    unit impulses through Chain.run give y[m] = kernel_taps[2 m + c - 3 p]
+    bitwise (0 outside the taps) -- every third output from the one-multiply
+    path, the others from the FMA chains -- at tile and sub-chunk edges."""
+    from dspcore import design
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    n = 4800
+    pos = [0, 1, 2, 31, 32, 2047, 2048, 2049, 4799]
+    x = np.zeros((len(pos), n), np.float32)
+    for r, p in enumerate(pos):
+        x[r, p] = 1.0
+    cfg = ChainConfig(n, 48000, 3, 2, None, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, len(pos), gpu)
+    assert ch.tile_len > 0
+    kt = design.kernel_taps(ch.src)
+    y = ch.run(torch.from_numpy(x).to(gpu))[0].cpu().numpy()
+    m = np.arange(ch.n_out)
+    for r, p in enumerate(pos):
+        k = 2 * m + ch.src.c_offset - 3 * p
+        want = np.where((k >= 0) & (k < ch.src.K), kt[np.clip(k, 0, ch.src.K - 1)], 0.0)
+        np.testing.assert_array_equal(y[r], want.astype(np.float32))
