@@ -368,7 +368,7 @@ def extra_line(wl, r, steps):
     }
 
 
-def host_inclusive(device, channels=1024, reps=3):
+def host_inclusive(device, channels=1024, reps=5):
     """SURVEY.md §8(d)'s host-inclusive rate: numpy x in, H2D, the chain
     (config-3/4 geometry, hand-off status checked), D2H of y, z and |Z|, numpy
     out -- what the drop-in path costs per call.  Never `value`.
@@ -389,10 +389,12 @@ def host_inclusive(device, channels=1024, reps=3):
     def timed(once):
         once()
         torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(reps):
+            t0 = time.perf_counter()
             once()
-        return (time.perf_counter() - t0) / reps
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]   # median: host-side stalls hit single calls
 
     chain = Chain(cfg, channels, device)
 
@@ -414,8 +416,8 @@ def host_inclusive(device, channels=1024, reps=3):
             "pcie_bytes_per_call": moved, "pcie_gbs": round(moved / wall / 1e9, 2),
             "how": "numpy x -> dspcore.host.HostChain (64-channel blocks, 4 slots: host copy into "
                    "pinned staging, H2D, dsp_chain_f32 (config-4 geometry), D2H of y, z, |Z| into "
-                   "pinned numpy outputs, overlapped) -> numpy, status checked; mean of 3 calls "
-                   "after 1 warm",
+                   "pinned numpy outputs, overlapped; staging copies on 4 threads) -> numpy, status "
+                   "checked; median of 5 calls after 1 warm",
             "single_call": {"value": round(channels * wl["n_in"] / wall1 / 1e6, 2),
                             "ms_per_call": round(wall1 * 1e3, 3),
                             "how": "pageable numpy -> torch H2D -> Chain.run -> .cpu().numpy() "

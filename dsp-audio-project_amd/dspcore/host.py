@@ -31,6 +31,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from concurrent.futures import ThreadPoolExecutor
+
 from .chain import Chain, ChainConfig
 
 
@@ -38,7 +40,7 @@ class HostChain:
     """Pipelined numpy -> device -> numpy runner of one ChainConfig."""
 
     def __init__(self, cfg: ChainConfig, device: torch.device | str = "cuda", block: int = 64,
-                 slots: int = 4, keep_y: bool = True):
+                 slots: int = 4, keep_y: bool = True, copy_threads: int = 4):
         if block < 1 or slots < 1:
             raise ValueError("block and slots must be >= 1")
         self.cfg = cfg
@@ -55,6 +57,10 @@ class HostChain:
         self.xdev = [torch.empty((self.block, n_in), dtype=torch.float32, device=self.device)
                      for _ in range(slots)]
         self.done: list = [None] * slots
+        # numpy releases the GIL in its copy loops: the copy into pinned staging
+        # runs on a few threads, row slices each
+        self._pool = ThreadPoolExecutor(copy_threads) if copy_threads > 1 else None
+        self._nthreads = max(1, int(copy_threads))
         self._out_B = -1
         self._out: tuple = ()
 
@@ -65,6 +71,16 @@ class HostChain:
             self._out = (y, torch.empty((B, self.n_out), **pin), torch.empty((B, self.n_mag), **pin))
             self._out_B = B
         return self._out
+
+    def _fill(self, xp: np.ndarray, x: np.ndarray, lo: int, nb: int) -> None:
+        if self._pool is None or nb < 2 * self._nthreads:
+            np.copyto(xp[:nb], x[lo:lo + nb])
+            return
+        step = -(-nb // self._nthreads)
+        futs = [self._pool.submit(np.copyto, xp[r:min(nb, r + step)], x[lo + r:lo + min(nb, r + step)])
+                for r in range(0, nb, step)]
+        for f in futs:
+            f.result()
 
     def run(self, x: np.ndarray, copy: bool = False):
         """y, z, |Z| (numpy float32, [B, n_out], [B, n_out], [B, n_fft/2+1]) of a
@@ -84,7 +100,7 @@ class HostChain:
             if self.done[s] is not None:
                 self.done[s].synchronize()  # the slot's previous block has left the device
             xp = self.xpin[s].numpy()
-            np.copyto(xp[:nb], x[lo:hi])
+            self._fill(xp, x, lo, nb)
             if nb < self.block:
                 xp[nb:] = 0.0
             st = self.streams[s]

@@ -20,8 +20,10 @@ cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], bench.
                   n_fft=wl["n_fft"])
 x = np.random.default_rng(5).uniform(-1, 1, (1024, wl["n_in"])).astype(np.float32)
 for spec in sys.argv[1:] or ["64:3", "64:4", "32:4", "128:3"]:
-    blk, sl = (int(v) for v in spec.split(":"))
-    hc = HostChain(cfg, dev, block=blk, slots=sl)
+    parts = [int(v) for v in spec.split(":")]
+    blk, sl = parts[0], parts[1]
+    th = parts[2] if len(parts) > 2 else 4
+    hc = HostChain(cfg, dev, block=blk, slots=sl, copy_threads=th)
     hc.run(x)
     ts = []
     for _ in range(5):
@@ -29,7 +31,7 @@ for spec in sys.argv[1:] or ["64:3", "64:4", "32:4", "128:3"]:
         hc.run(x)
         ts.append(time.perf_counter() - t0)
     w = float(np.median(ts))
-    print(f"block {blk} slots {sl}: median {w * 1e3:.2f} ms, {1024 * 48000 / w / 1e6:.1f} "
+    print(f"block {blk} slots {sl} threads {th}: median {w * 1e3:.2f} ms, {1024 * 48000 / w / 1e6:.1f} "
           f"Msamples/s (min {min(ts) * 1e3:.2f} max {max(ts) * 1e3:.2f})", flush=True)
     del hc
     torch.cuda.empty_cache()
