@@ -408,6 +408,7 @@ def host_inclusive(device, channels=1024, reps=5):
     torch.cuda.empty_cache()
     hc = HostChain(cfg, device, block=64, slots=4)
     wall = timed(lambda: hc.run(x))
+    hc.close()
     del hc
     torch.cuda.empty_cache()
     moved = x.nbytes + 2 * 4 * channels * n_out + 4 * channels * (wl["n_fft"] // 2 + 1)

@@ -72,6 +72,23 @@ class HostChain:
             self._out_B = B
         return self._out
 
+    def close(self) -> None:
+        """Stops the staging-copy threads (the device buffers go with the object)."""
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.shutdown(wait=False)
+
     def _fill(self, xp: np.ndarray, x: np.ndarray, lo: int, nb: int) -> None:
         if self._pool is None or nb < 2 * self._nthreads:
             np.copyto(xp[:nb], x[lo:lo + nb])

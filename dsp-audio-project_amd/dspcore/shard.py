@@ -102,6 +102,8 @@ def run_sharded_host(cfg, x: np.ndarray, devices: list | None = None, block: int
         t.start()
     for t in threads:
         t.join()
+    for r in runners:
+        r.close()
     if errors:
         raise errors[0]
     return y, z, mag
