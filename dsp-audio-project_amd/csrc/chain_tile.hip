@@ -95,6 +95,9 @@ constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 // Config 5 (160/147): k_chain_gct; -DDSP_C5_G5=1 builds the class-uniform
 // k_chain_g5 instead (measured 22 % slower).
+#ifndef DSP_SRC_PARTS
+X
+#endif
 #ifndef DSP_GCT_T7
 #define DSP_GCT_T7 1  // 0: every output reads and FMAs all 5 tap pairs (A/B builds)
 #endif
@@ -942,6 +945,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   {
     const float* xw = lds + 36 * lane;
     static_assert(TS == 48, "four parts");
+#if DSP_SRC_PARTS == 2
+    src_part<GEO, 0, 24, DLY>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 24, 24, DLY>(xw, mt, y);
+    pin(y);
+#elif DSP_SRC_PARTS == 3
+    src_part<GEO, 0, 16, DLY>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 16, 16, DLY>(xw, mt, y);
+    pin(y);
+    src_part<GEO, 32, 16, DLY>(xw, mt, y);
+    pin(y);
+#else
     src_part<GEO, 0, 12, DLY>(xw, mt, y);
     pin(y);
     src_part<GEO, 12, 12, DLY>(xw, mt, y);
@@ -950,6 +966,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     pin(y);
     src_part<GEO, 36, 12, DLY>(xw, mt, y);
     pin(y);
+#endif
   }
   tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
 }
