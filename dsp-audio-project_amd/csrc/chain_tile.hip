@@ -96,7 +96,8 @@ constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 // Config 5 (160/147): k_chain_gct; -DDSP_C5_G5=1 builds the class-uniform
 // k_chain_g5 instead (measured 22 % slower).
 #ifndef DSP_SRC_PARTS
-X
+#define DSP_SRC_PARTS 2  // k_chain_tile's SRC in 2 parts of 24 outputs (3, 4: parts of 16, 12;
+                         // 4 was the default before the delay branch freed the registers)
 #endif
 #ifndef DSP_GCT_T7
 #define DSP_GCT_T7 1  // 0: every output reads and FMAs all 5 tap pairs (A/B builds)
