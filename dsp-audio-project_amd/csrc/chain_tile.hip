@@ -99,6 +99,10 @@ constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 #define DSP_SRC_PARTS 2  // k_chain_tile's SRC in 2 parts of 24 outputs (3, 4: parts of 16, 12;
                          // 4 was the default before the delay branch freed the registers)
 #endif
+#ifndef DSP_SRC_PARTS_DLY
+#define DSP_SRC_PARTS_DLY 1  // the DLY kernel's SRC in one part of 48 (its 16 delay outputs need
+                             // no accumulators: 128 VGPRs, no scratch; without DLY one part spills)
+#endif
 #ifndef DSP_GCT_T7
 #define DSP_GCT_T7 1  // 0: every output reads and FMAs all 5 tap pairs (A/B builds)
 #endif
@@ -946,7 +950,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   {
     const float* xw = lds + 36 * lane;
     static_assert(TS == 48, "four parts");
-#if DSP_SRC_PARTS == 2
+#if DSP_SRC_PARTS == 1 || DSP_SRC_PARTS_DLY == 1
+    if constexpr (DLY || DSP_SRC_PARTS == 1) {
+      src_part<GEO, 0, 48, DLY>(xw, mt, y);
+      pin(y);
+    } else {
+      src_part<GEO, 0, 24, DLY>(xw, mt, y);
+      pin(y);
+      src_part<GEO, 24, 24, DLY>(xw, mt, y);
+      pin(y);
+    }
+#elif DSP_SRC_PARTS == 2
     src_part<GEO, 0, 24, DLY>(xw, mt, y);
     pin(y);
     src_part<GEO, 24, 24, DLY>(xw, mt, y);
