@@ -27,11 +27,10 @@
 //      then one float64 change of basis E'_l = Q e_l, Q = T^-1 P (lower
 //      triangular, 78 FMAs per lane), into block-diagonal coordinates (below);
 //   3. carry: the tile's entry state m_in comes from the previous tile of the
-//      same channel (chained hand-off, below); an inclusive Kogge-Stone scan
-//      across the 64 lanes, v_l += D^(TSUB 2^d) v_(l-2^d) for d = 0..5, gives
-//      every sub-chunk's entry state m_l = v_(l-1) (m_0 = m_in, folded into
-//      lane 0 as v_0 = D^TSUB m_in + E'_0);
-//   4. lane 63's v (the tile's end state) is published for the next tile;
+//      same channel (chained hand-off, below); a blocked scan of the 64
+//      lanes' E' through LDS (tile_cascade) gives every sub-chunk's entry
+//      state m_l = v_(l-1), v_l = D^TSUB v_(l-1) + E'_l, v_(-1) = m_in;
+//   4. v_63 (the tile's end state) is published for the next tile;
 //   5. y leaves through LDS as coalesced float4 stores; the lane's DF2 state
 //      is s_l = T m_l and pass 2 reruns the cascade over the sub-chunk from it,
 //      clips, and z leaves the same way.
@@ -64,8 +63,7 @@
 // release/acquire: the memory model's agent-scope release/acquire fences add
 // buffer_wbl2 sc1 / buffer_inv sc1 (L2 write-back / invalidate), which the
 // atomics do not need and which measured 5.8x slower (config 4: 37.7 vs
-// 6.55 ms, profiles/r03_handoff_fence_ab.txt; -DDSP_HANDOFF_FENCED=1 builds
-// that variant).  The consumer clears the flag, so a completed launch leaves
+// 6.55 ms, profiles/r03_handoff_fence_ab.txt).  The consumer clears the flag, so a completed launch leaves
 // the flag array zero for the next one (the caller zero-fills the workspace
 // once).  A wait that polls more than the thread's spin limit
 // (dsp_chain_spin_limit; default 2^23 polls with s_sleep 2 between them,
@@ -93,22 +91,6 @@ constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
-// Config 5 (160/147): k_chain_gct; -DDSP_C5_G5=1 builds the class-uniform
-// k_chain_g5 instead (measured 22 % slower).
-#ifndef DSP_SRC_PARTS
-#define DSP_SRC_PARTS 2  // k_chain_tile's SRC in 2 parts of 24 outputs (3, 4: parts of 16, 12;
-                         // 4 was the default before the delay branch freed the registers)
-#endif
-#ifndef DSP_SRC_PARTS_DLY
-#define DSP_SRC_PARTS_DLY 1  // the DLY kernel's SRC in one part of 48 (its 16 delay outputs need
-                             // no accumulators: 128 VGPRs, no scratch; without DLY one part spills)
-#endif
-#ifndef DSP_GCT_T7
-#define DSP_GCT_T7 1  // 0: every output reads and FMAs all 5 tap pairs (A/B builds)
-#endif
-#ifndef DSP_C5_G5
-#define DSP_C5_G5 0
-#endif
 constexpr int kScanRow = 14;  // doubles per row of the blocked carry scan (12 used)
 constexpr int kScanFloats = 66 * kScanRow * 2;  // its LDS: 64 rows + row 64 + the park row
 
@@ -205,14 +187,6 @@ struct TileTables {
   // shift s_i = (i M div L) mod 2 + (1 if the class's phase carries q one
   // further, else 0), zero outside the T taps.
   alignas(16) float seqs[kGenClasses][kGenTS][kCtRow];
-  // k_chain_tile with the SRC on the matrix cores (DSP_SRC_MFMA): the tile's
-  // SRC as Y[48 x 64] = H[48 x 80] X[80 x 64] (H: output i's taps at window
-  // offsets, X: lane n's window in column n), the taps scaled by 2^hexp and
-  // split into two float16 planes (hi + lo), as the A operands of
-  // v_mfma_f32_16x16x32_f16 in lane order: Hmf[mt][ks][plane][lane][j] =
-  // H[16 mt + lane % 16][k0(mt) + 32 ks + 8 (lane / 16) + j] (k0 = 8 mt).
-  alignas(16) _Float16 Hmf[3][2][2][64][8];
-  int32_t hexp, pad2;
 };
 
 struct TileArgs {
@@ -390,26 +364,6 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
   fence();
 }
 
-// A/B variant (-DDSP_DIRECT_STORE=1): each lane stores its own TS outputs as
-// float4s straight from registers (no LDS staging; a wave-instruction then
-// writes 16 B per lane at a TS*4-byte lane stride, and the lines fill over
-// TS/4 instructions).
-template <int TS>
-__device__ __forceinline__ void store_direct(const float (&v)[TS], int lane,
-                                             __amdgpu_buffer_rsrc_t rs, int64_t m0) {
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const int64_t base = (m0 + (int64_t)lane * TS) * 4;
-#pragma unroll
-  for (int k = 0; k < TS / 4; ++k) {
-    u32x4 d;
-    d.x = __float_as_uint(v[4 * k]);
-    d.y = __float_as_uint(v[4 * k + 1]);
-    d.z = __float_as_uint(v[4 * k + 2]);
-    d.w = __float_as_uint(v[4 * k + 3]);
-    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)base, 16 * k, kStream);
-  }
-}
-
 // Entry state of the tile: lane 0 waits for the previous tile of the channel
 // (hand-off, file comment) and loads its end state; zero for tile 0 and for
 // the other lanes.
@@ -431,9 +385,6 @@ __device__ __forceinline__ void tile_entry_state(const TileArgs& a, int64_t b, i
       }
       __builtin_amdgcn_s_sleep(2);
     }
-#if DSP_HANDOFF_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     fence();
 #pragma unroll
     for (int d = 0; d < kD; ++d) m_in[d] = load_state(a.states + prev * kD + d);
@@ -449,17 +400,6 @@ __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * 
 // input-normal coordinates, one float64 change of basis).
 template <int TS>
 __device__ __forceinline__ void pass1_state(tt_ptr mt, const float (&y)[TS], double (&v)[kD]) {
-#if DSP_P1_F64
-  // float64 sums in block-diagonal coordinates (round 2; A/B reference)
-#pragma unroll
-  for (int d = 0; d < kD; ++d) v[d] = 0.0;
-#pragma unroll
-  for (int i = 0; i < TS; ++i) {
-    const double u = (double)y[i];
-#pragma unroll
-    for (int d = 0; d < kD; ++d) v[d] = fma(mt->G[i][d], u, v[d]);
-  }
-#else
   {
     // float32 sums in input-normal coordinates: component d keeps the sums
     // over even and odd samples in the halves of one v_pk_fma_f32 chain
@@ -502,7 +442,6 @@ __device__ __forceinline__ void pass1_state(tt_ptr mt, const float (&y)[TS], dou
       v[r] = acc;
     }
   }
-#endif
 }
 
 // Pass 2 (file comment, step 5): DF2 entry state s = T m, the cascade rerun
@@ -565,60 +504,6 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   pin(v);
 
   // ---- 3. entry state of the tile and the scan across the lanes
-#if DSP_SCAN_KS
-  double m_in[kD];
-  tile_entry_state(a, b, tile, lane, m_in);
-  if (tile > 0 && lane == 0) {
-    // v_0 = D^TSUB m_in + E'_0
-#pragma unroll
-    for (int k = 0; k < kS; ++k)
-      mac2(mt->Dp[0][k], m_in[2 * k], m_in[2 * k + 1], v[2 * k], v[2 * k + 1]);
-  }
-  // Kogge-Stone scan over the 64 lanes with ds_bpermute (round 2; A/B build).
-  // m_in waits out the scan in LDS (free until the y store), not in 24 VGPRs
-  // of every lane at the kernel's register peak.
-  double* park = reinterpret_cast<double*>(lds);
-  if (lane == 0) {
-#pragma unroll
-    for (int d = 0; d < kD; ++d) park[d] = m_in[d];
-  }
-  fence();
-#pragma unroll
-  for (int lv = 0; lv < 6; ++lv) {
-    const int off = 1 << lv;
-    double x[kD];
-#pragma unroll
-    for (int d = 0; d < kD; ++d) x[d] = shfl_up_f64(v[d], off);
-    if (lane >= off) {
-#pragma unroll
-      for (int k = 0; k < kS; ++k) mac2(mt->Dp[lv][k], x[2 * k], x[2 * k + 1], v[2 * k], v[2 * k + 1]);
-    }
-  }
-  // Entry state of the lane's sub-chunk: v of the lane before (m_in for lane 0).
-  double m[kD];
-#pragma unroll
-  for (int d = 0; d < kD; ++d) m[d] = shfl_up_f64(v[d], 1);
-  fence();
-  if (lane == 0) {
-#pragma unroll
-    for (int d = 0; d < kD; ++d) m[d] = park[d];
-  }
-  fence();
-
-  // ---- 4. publish the tile's end state (lane 63) for the next tile
-  if (tile + 1 < a.ntiles && lane == kWave - 1) {
-    const int64_t me = b * a.ntiles + tile;
-#pragma unroll
-    for (int d = 0; d < kD; ++d) store_state(a.states + me * kD + d, v[d]);
-#if DSP_HANDOFF_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    store_flag(a.flags + me, 1u);
-  }
-
-#else
   // Blocked scan through LDS.  Rows r = 0..63 take E'_r (row stride kScanRow
   // doubles: the b128 accesses of 16 lanes hit 16 distinct bank quads); 48
   // worker lanes, one per (state block k, segment s of 8 rows), run the
@@ -720,11 +605,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       store_state(a.states + me * kD + 2 * kb, u0);
       store_state(a.states + me * kD + 2 * kb + 1, u1);
     }
-#if DSP_HANDOFF_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     if (lane == 8 * 7) store_flag(a.flags + me, 1u);
   }
   fence();
@@ -739,18 +620,13 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     }
   }
   fence();
-#endif  // DSP_SCAN_KS
 
   // ---- 5. y out (unless the caller passed y = NULL), DF2 entry state
   // s = T m, pass 2, z out
   if (YST && a.y) {
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
         a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-#if DSP_DIRECT_STORE
-    store_direct<TS>(y, lane, ry, m0);
-#else
     store_tile<TS>(lds, y, lane, ry, m0);
-#endif
   }
   pin(y);
   pass2_cascade<TS>(a, mt, y, m);
@@ -758,164 +634,9 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   int lane_z = lane;
   asm volatile("" : "+v"(lane_z));  // recompute the store offsets (no spill across pass 2)
-#if DSP_DIRECT_STORE
-  store_direct<TS>(y, lane_z, rz, m0);
-#else
   store_tile<TS>(lds, y, lane_z, rz, m0);
-#endif
 }
 
-#if DSP_SRC_MFMA
-// ---------------------------------------------------------------------------
-// SRC on the matrix cores (A/B build, -DDSP_SRC_MFMA=1).  Y[48 x 64] = H X
-// per tile as 3 (M) x 4 (N) x 2 (K) v_mfma_f32_16x16x32_f16 tiles, each
-// operand split into float16 hi + lo (x scaled by a power of two per wave so
-// that max|x| lands in [2^14, 2^15), the taps by 2^hexp on the host) and the
-// four products lo*lo, lo*hi, hi*lo, hi*hi accumulated in float32: the split
-// keeps 22 of float32's 24 bits per operand, the error of the sums is that of
-// float32 FMAs (tools/sim_split.py).  x goes to LDS once as the two planes
-// (16-B chunks XOR-swizzled: the B-operand reads of 16 lanes hit 16 distinct
-// bank quads); the result tiles are transposed through the same LDS into the
-// y store's staging rows, from which every lane also takes its 48 outputs.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-constexpr int kMfWin = 32 * 63 + 16 + 64;       // window samples the B operands read
-constexpr int kMfPlane = (kMfWin / 8 + 15) / 16 * 16 * 8;  // halfs per plane (whole swizzle groups)
-__device__ __forceinline__ int mf_chunk(int c) { return c ^ ((c >> 4) & 3); }
-
-template <class GEO, bool DLY = false>  // (DLY: the VALU SRC's shortcut; unused here)
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
-    TileArgs a) {
-  constexpr int TS = GEO::TSUB;
-  static_assert(TS == 48 && GEO::L == 3 && GEO::M == 2, "matrix-core SRC: the L3/M2 tile");
-  static_assert(staging_floats(TS) * 4 <= 2 * kMfPlane * 2 && kScanFloats <= kMfPlane,
-                "staging and scan rows fit the planes");
-  __shared__ __attribute__((aligned(16))) float lds[kMfPlane];  // 2 planes of kMfPlane halfs
-  const int lane = threadIdx.x;
-  const int64_t id = blockIdx.x;
-  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
-  const int64_t m0 = tile * GEO::TILE;
-  const tt_ptr mt = (tt_ptr)a.tt;
-  char* const pl0 = reinterpret_cast<char*>(lds);
-  char* const pl1 = pl0 + kMfPlane * 2;
-
-  // ---- x window -> registers, wave max|x|, split into f16 planes in LDS
-  {
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
-    const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);
-    constexpr int NF = kMfWin / 4;
-    constexpr int NK = (NF + kWave - 1) / kWave;
-    f32x4 v[NK];
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      const int f = lane + kWave * k;
-      v[k] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, kStream);
-    }
-    float mx = 0.f;
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-      mx = fmaxf(fmaxf(fmaxf(mx, fabsf(v[k].x)), fmaxf(fabsf(v[k].y), fabsf(v[k].z))), fabsf(v[k].w));
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-    const int ex = (int)((__float_as_uint(mx) >> 23) & 255);
-    int sx = (ex == 0 || ex == 255) ? 0 : 141 - ex;  // max|x| * 2^sx in [2^14, 2^15)
-    sx = __builtin_amdgcn_readfirstlane(sx < -100 ? -100 : (sx > 100 ? 100 : sx));
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      const int f = lane + kWave * k;
-      if ((k + 1) * kWave <= NF || f < NF) {
-        const float x0 = __builtin_ldexpf(v[k].x, sx), x1 = __builtin_ldexpf(v[k].y, sx);
-        const float x2 = __builtin_ldexpf(v[k].z, sx), x3 = __builtin_ldexpf(v[k].w, sx);
-        const f16x2 h01 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(x0, x1));
-        const f16x2 h23 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(x2, x3));
-        const f16x2 l01 = __builtin_bit_cast(
-            f16x2, __builtin_amdgcn_cvt_pkrtz(x0 - (float)h01.x, x1 - (float)h01.y));
-        const f16x2 l23 = __builtin_bit_cast(
-            f16x2, __builtin_amdgcn_cvt_pkrtz(x2 - (float)h23.x, x3 - (float)h23.y));
-        const int off = (mf_chunk(f >> 1) << 4) + ((f & 1) << 3);
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2*>(pl0 + off) =
-            u32x2{__builtin_bit_cast(unsigned int, h01), __builtin_bit_cast(unsigned int, h23)};
-        *reinterpret_cast<u32x2*>(pl1 + off) =
-            u32x2{__builtin_bit_cast(unsigned int, l01), __builtin_bit_cast(unsigned int, l23)};
-      }
-    }
-    fence();
-    // ---- 1. SRC: 12 result tiles of 16 outputs x 16 sub-chunks
-    f32x4 acc[3][4];
-    const f16x8* Ag = reinterpret_cast<const f16x8*>(&a.tt->Hmf[0][0][0][0][0]);
-    const int la = lane & 15, lb = lane >> 4;
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      f16x8 A[2][2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) A[ks][p] = Ag[((m * 2 + ks) * 2 + p) * kWave + lane];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int chunk = (32 * (16 * n + la) + 8 * m + 32 * ks + 8 * lb) >> 3;
-          const int off = mf_chunk(chunk) << 4;
-          const f16x8 Bh = *reinterpret_cast<const f16x8*>(pl0 + off);
-          const f16x8 Bl = *reinterpret_cast<const f16x8*>(pl1 + off);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][1], Bl, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][1], Bh, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][0], Bl, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ks][0], Bh, c, 0, 0, 0);
-        }
-        const int sc = -(sx + mt->hexp);
-        acc[m][n] = f32x4{__builtin_ldexpf(c.x, sc), __builtin_ldexpf(c.y, sc),
-                          __builtin_ldexpf(c.z, sc), __builtin_ldexpf(c.w, sc)};
-      }
-    }
-    fence();
-    // ---- y out and every lane's 48 outputs: per half of the sub-chunks, the
-    // tiles go to the staging rows (row = sub-chunk, stride TS + 4), the half
-    // leaves as coalesced float4s, and its lanes read their rows back.
-    float y[TS];
-    constexpr int RS = TS + 4;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int n = 2 * h; n < 2 * h + 2; ++n)
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-          *reinterpret_cast<f32x4*>(lds + (16 * (n - 2 * h) + la) * RS + 16 * m + 4 * lb) = acc[m][n];
-      fence();
-      if (a.y) {
-#pragma unroll
-        for (int k = 0; k < (kWave / 2) * TS / 4 / kWave; ++k) {
-          const int g = 4 * (lane + kWave * k);
-          const int r = g / TS, cc = g - r * TS;
-          const f32x4 f = *reinterpret_cast<const f32x4*>(lds + r * RS + cc);
-          const int64_t off = (m0 + (int64_t)h * (kWave / 2) * TS + g) * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), ry, (int)off, 0, kStream);
-        }
-      }
-      if ((lane >> 5) == h) {
-#pragma unroll
-        for (int k = 0; k < TS / 4; ++k) {
-          const f32x4 f = *reinterpret_cast<const f32x4*>(lds + (lane & 31) * RS + 4 * k);
-          y[4 * k] = f.x;
-          y[4 * k + 1] = f.y;
-          y[4 * k + 2] = f.z;
-          y[4 * k + 3] = f.w;
-        }
-      }
-      fence();
-    }
-    pin(y);
-    tile_cascade<TS, false>(a, mt, lds, y, lane, b, tile, m0);
-  }
-}
-#else
 template <class GEO, bool DLY = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
@@ -945,48 +666,25 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   }
   fence();  // one wave: its LDS operations execute in order
 
-  // ---- 1. SRC: the lane's TSUB outputs, in parts of 12 (register pressure)
+  // ---- 1. SRC: the lane's TSUB outputs, in parts (register pressure)
   float y[TS];
   {
     const float* xw = lds + 36 * lane;
-    static_assert(TS == 48, "four parts");
-#if DSP_SRC_PARTS == 1 || DSP_SRC_PARTS_DLY == 1
-    if constexpr (DLY || DSP_SRC_PARTS == 1) {
-      src_part<GEO, 0, 48, DLY>(xw, mt, y);
+    static_assert(TS == 48, "SRC parts of 48 / 24 outputs");
+    // DLY: one part of 48 (its delay outputs need no accumulators: 128 VGPRs,
+    // no scratch); the plain kernel in two parts of 24 (one part would spill).
+    if constexpr (DLY) {
+      src_part<GEO, 0, 48, true>(xw, mt, y);
       pin(y);
     } else {
-      src_part<GEO, 0, 24, DLY>(xw, mt, y);
+      src_part<GEO, 0, 24, false>(xw, mt, y);
       pin(y);
-      src_part<GEO, 24, 24, DLY>(xw, mt, y);
+      src_part<GEO, 24, 24, false>(xw, mt, y);
       pin(y);
     }
-#elif DSP_SRC_PARTS == 2
-    src_part<GEO, 0, 24, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 24, 24, DLY>(xw, mt, y);
-    pin(y);
-#elif DSP_SRC_PARTS == 3
-    src_part<GEO, 0, 16, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 16, 16, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 32, 16, DLY>(xw, mt, y);
-    pin(y);
-#else
-    src_part<GEO, 0, 12, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 12, 12, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 24, 12, DLY>(xw, mt, y);
-    pin(y);
-    src_part<GEO, 36, 12, DLY>(xw, mt, y);
-    pin(y);
-#endif
   }
   tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
 }
-
-#endif  // DSP_SRC_MFMA
 
 // ---------------------------------------------------------------------------
 // Generic single-pass kernel: any L, M with ceil(K/L) <= 8 (config 5's
@@ -1230,292 +928,12 @@ k_chain_gct(TileArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Config-5 kernel with class-uniform waves (k_chain_g5<L, M>, round 3; an A/B
-// build, -DDSP_C5_G5=1: measured 1.54 vs 1.26 ms for k_chain_gct at config 5,
-// profiles/r03_c5_g5_ab.txt).  Sub-chunks
-// of 32 outputs repeat their polyphase pattern with period C = 5 (the phase
-// classes, k_chain_gen's comment), so a workgroup of C waves takes a tile of
-// 64 C = 320 consecutive sub-chunks (10240 outputs) of one channel and wave w
-// computes the sub-chunks j = 5 l + w of class w: its taps are wave-uniform,
-// read through the scalar cache (no tap rows in LDS), and the five waves share
-// one x window.  SRC (same FMA order as k_chain_gct, so y is bitwise the same)
-// and pass 1 per lane; the carry is the blocked scan over the tile's 320 rows:
-// wave w scans segments 8 w .. 8 w + 7 (as tile_cascade), writes its group
-// total, and after one barrier takes its group's entry state from the totals
-// of the waves before it (<= 4 block steps, D^(64 TSUB) by squaring); the
-// segment entry adds D^(8 TSUB s) of it (Dp[3..5], by the bits of s).  Each
-// wave stages its y and z stores in its own LDS slice (half a wave of rows at
-// a time): one row = one sub-chunk = one 128-byte line.
-// ---------------------------------------------------------------------------
-constexpr int kG5Waves = 5;                               // = phase classes (160/147)
-#ifndef G5_TAPBLK
-#define G5_TAPBLK 1
-#endif
-constexpr int kG5Sub = kWave * kG5Waves;                  // sub-chunks per tile
-constexpr int kG5Tile = kG5Sub * kGenTS;                  // outputs per tile
-constexpr int kG5ScanFloats = ((kG5Sub + 2) * kScanRow + kG5Waves * kD) * 2;
-constexpr int kG5StageFloats = kG5Waves * staging_floats(kGenTS);
-
-// Stores a wave's 64 sub-chunks (lane l: sub-chunk 5 l + w, TS = 32 outputs)
-// through its staging slice: per half of the lanes, rows (stride TS + 4) into
-// LDS, then 8 lanes per row read them back and store the row's 128 bytes.
-__device__ __forceinline__ void g5_store(float* stage, const float (&v)[kGenTS], int lane, int w,
-                                         __amdgpu_buffer_rsrc_t rs, int64_t m0) {
-  constexpr int TS = kGenTS, RS = TS + 4;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    fence();
-    if ((lane >> 5) == h) {
-      float* row = stage + (lane & 31) * RS;
-#pragma unroll
-      for (int k = 0; k < TS / 4; ++k)
-        *reinterpret_cast<float4*>(row + 4 * k) =
-            make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
-    fence();
-#pragma unroll
-    for (int k = 0; k < (kWave / 2) * TS / 4 / kWave; ++k) {
-      const int g = 4 * (lane + kWave * k);
-      const int r = g / TS, c = g - r * TS;
-      const float4 f = *reinterpret_cast<const float4*>(stage + r * RS + c);
-      u32x4 d;
-      d.x = __float_as_uint(f.x);
-      d.y = __float_as_uint(f.y);
-      d.z = __float_as_uint(f.z);
-      d.w = __float_as_uint(f.w);
-      const int64_t j = (int64_t)kG5Waves * (r + (kWave / 2) * h) + w;
-      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)((m0 + TS * j + c) * 4), 0, kStream);
-    }
-  }
-  fence();
-}
-
-template <int L, int M>
-__global__ __launch_bounds__(kWave * kG5Waves) __attribute__((amdgpu_waves_per_eu(5))) void
-k_chain_g5(TileArgs a) {
-  static_assert(M < L, "q advances by 0 or 1 per output");
-  constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
-  typedef double f64x2 __attribute__((ext_vector_type(2)));
-  typedef const __attribute__((address_space(1))) double* gdp;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t id = blockIdx.x;
-  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major, one channel per workgroup
-  const int T = a.T;
-  const tt_ptr mt = (tt_ptr)a.tt;
-  const int64_t m0 = tile * kG5Tile;
-  const int j = kG5Waves * lane + w;  // the lane's sub-chunk within the tile (class w)
-
-  // ---- x window of the tile: x[qa .. qa + win) (zeros outside [0, n_in))
-  const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
-  const int64_t qa = (qlo >> 2) << 2;
-  {
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
-    const int nf = a.win >> 2;
-    for (int f0 = 0; f0 < nf; f0 += 8 * kG5Sub) {
-      f32x4 v[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kG5Sub + (int)threadIdx.x;  // past the window: harmless reads
-        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kG5Sub + (int)threadIdx.x;
-        if (f < nf) *reinterpret_cast<f32x4*>(smem + 4 * f) = v[r];
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- 1. SRC of the lane's 32 outputs; class w's taps from the scalar cache
-  float y[kGenTS];
-  {
-    const int64_t j0 = (m0 + (int64_t)kGenTS * j) * M + a.c;
-    const float* xl = smem + (int)(j0 / L - (T - 1) - qa);
-    f32x2 X[NPW];
-#pragma unroll
-    for (int mm = 0; mm < NPW; ++mm) X[mm] = f32x2{xl[2 * mm], xl[2 * mm + 1]};
-    // one opaque table pointer per G5_TAPBLK outputs: their rows' scalar
-    // loads are issued together (fewer lgkmcnt waits, more SGPRs)
-    tt_ptr tq = mt;
-#pragma unroll
-    for (int i = 0; i < kGenTS; ++i) {
-      if (i % G5_TAPBLK == 0) asm volatile("" : "+s"(tq));
-      const auto* t = &tq->seqs[w][i][0];
-      const int g2 = (i * M / L) / 2;
-      f32x2 acc = {0.f, 0.f};
-      acc = __builtin_elementwise_fma(f32x2{t[0], t[1]}, X[g2], acc);
-      acc = __builtin_elementwise_fma(f32x2{t[2], t[3]}, X[g2 + 1], acc);
-      acc = __builtin_elementwise_fma(f32x2{t[4], t[5]}, X[g2 + 2], acc);
-      acc = __builtin_elementwise_fma(f32x2{t[6], t[7]}, X[g2 + 3], acc);
-      acc = __builtin_elementwise_fma(f32x2{t[8], t[9]}, X[g2 + 4], acc);
-      y[i] = acc.x + acc.y;
-    }
-  }
-  pin(y);
-  __syncthreads();  // the x window is dead: its LDS becomes the scan rows
-
-  // ---- 2. pass 1, rows, the tile's entry state
-  double* rows = reinterpret_cast<double*>(smem);
-  double* park = rows + (kG5Sub + 1) * kScanRow;
-  double* gtot = rows + (kG5Sub + 2) * kScanRow;  // [wave][12] group totals
-  {
-    double v[kD];
-    pass1_state<kGenTS>(mt, y, v);
-    pin(v);
-#pragma unroll
-    for (int k = 0; k < kS; ++k)
-      *reinterpret_cast<f64x2*>(rows + j * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
-  }
-  if (w == 0) {
-    double m_in[kD];
-    tile_entry_state(a, b, tile, lane, m_in);
-    if (lane == 0) {
-#pragma unroll
-      for (int d = 0; d < kD; ++d) park[d] = m_in[d];
-    }
-  }
-  __syncthreads();
-
-  // ---- 3. blocked scan over the tile's 320 rows (tile_cascade's, per wave
-  // on its group of 64 rows, plus the group carry between the waves)
-  const int sg = lane >> 3;
-  const bool worker = (lane & 7) < 6;
-  const int kb = worker ? (lane & 7) : 0;
-  const int r0 = kWave * w + 8 * sg;  // the segment's first row
-  const gdp Dg = (gdp)&a.tt->Dp[0][kb][0];
-  const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
-  const f64x2 d0b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 2);
-  f64x2 p8a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 3 * kS * 4);
-  f64x2 p8b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 3 * kS * 4 + 2);
-  double u0 = 0.0, u1 = 0.0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const f64x2 ei = *reinterpret_cast<const f64x2*>(rows + (r0 + i) * kScanRow + 2 * kb);
-    if (i == 0) {
-      u0 = ei.x;
-      u1 = ei.y;
-      continue;
-    }
-    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, ei.x));
-    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, ei.y));
-    u0 = n0;
-    u1 = n1;
-  }
-  f64x2 mi = f64x2{0.0, 0.0};  // entry of the wave's first segment (m_in for wave 0)
-  if (w == 0 && sg == 0) {
-    mi = *reinterpret_cast<const f64x2*>(park + 2 * kb);
-    u0 = fma(p8a.x, mi.x, fma(p8a.y, mi.y, u0));
-    u1 = fma(p8b.x, mi.x, fma(p8b.y, mi.y, u1));
-  }
-#pragma unroll
-  for (int lv = 0; lv < 3; ++lv) {
-    const int dd = 1 << lv;
-    const int ss = sg - dd;
-    const int src = ss >= 0 ? lane - 8 * dd : lane;
-    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
-    if (ss >= 0) {
-      u0 = fma(p8a.x, x0, fma(p8a.y, x1, u0));
-      u1 = fma(p8b.x, x0, fma(p8b.y, x1, u1));
-    }
-    // D^(8 TSUB 2^(lv+1)); after the loop p8 = D^(64 TSUB), the group step
-    const f64x2 qa2 = f64x2{fma(p8a.x, p8a.x, p8a.y * p8b.x), fma(p8a.x, p8a.y, p8a.y * p8b.y)};
-    const f64x2 qb2 = f64x2{fma(p8b.x, p8a.x, p8b.y * p8b.x), fma(p8b.x, p8a.y, p8b.y * p8b.y)};
-    p8a = qa2;
-    p8b = qb2;
-  }
-  if (worker && sg == 7) *reinterpret_cast<f64x2*>(gtot + w * kD + 2 * kb) = f64x2{u0, u1};
-  {
-    const int ss = sg - 1;
-    const int src = ss >= 0 ? lane - 8 : lane;
-    const double x0 = shfl_f64(u0, src), x1 = shfl_f64(u1, src);
-    u0 = ss >= 0 ? x0 : mi.x;
-    u1 = ss >= 0 ? x1 : mi.y;
-  }
-  __syncthreads();  // group totals
-  if (w > 0) {
-    // entry of group w: P = sum over the groups before it, P <- D^(64 TSUB) P + G
-    f64x2 P = *reinterpret_cast<const f64x2*>(gtot + 2 * kb);
-    for (int g = 1; g < w; ++g) {
-      const f64x2 G = *reinterpret_cast<const f64x2*>(gtot + g * kD + 2 * kb);
-      P = f64x2{fma(p8a.x, P.x, fma(p8a.y, P.y, G.x)), fma(p8b.x, P.x, fma(p8b.y, P.y, G.y))};
-    }
-    // ... carried to the segment's start: D^(8 TSUB sg) P by the bits of sg
-#pragma unroll
-    for (int bit = 0; bit < 3; ++bit) {
-      if ((sg >> bit) & 1) {
-        const gdp Db = Dg + (3 + bit) * kS * 4;
-        const f64x2 ra = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Db);
-        const f64x2 rb = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Db + 2);
-        P = f64x2{fma(ra.x, P.x, ra.y * P.y), fma(rb.x, P.x, rb.y * P.y)};
-      }
-    }
-    u0 += P.x;
-    u1 += P.y;
-  }
-  // rerun the segment from its entry state, in place: each worker reads its
-  // block of row r (E'_r) and overwrites it with v_r; no other lane or wave
-  // touches that block (so row j - 1 holds sub-chunk j's entry state)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    f64x2* rp = reinterpret_cast<f64x2*>(rows + (r0 + i) * kScanRow + 2 * kb);
-    const f64x2 ei = *rp;
-    const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, ei.x));
-    const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, ei.y));
-    u0 = n0;
-    u1 = n1;
-    if (worker) *rp = f64x2{u0, u1};
-  }
-  // ---- 4. publish the tile's end state (the last wave's segment-7 workers)
-  if (w == kG5Waves - 1 && tile + 1 < a.ntiles) {
-    const int64_t me = b * a.ntiles + tile;
-    if (worker && sg == 7) {
-      store_state(a.states + me * kD + 2 * kb, u0);
-      store_state(a.states + me * kD + 2 * kb + 1, u1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 8 * 7) store_flag(a.flags + me, 1u);
-  }
-  __syncthreads();  // rows complete
-  double m[kD];
-  {
-    const double* src = j == 0 ? park : rows + (j - 1) * kScanRow;
-#pragma unroll
-    for (int k = 0; k < kS; ++k) {
-      const f64x2 t = *reinterpret_cast<const f64x2*>(src + 2 * k);
-      m[2 * k] = t.x;
-      m[2 * k + 1] = t.y;
-    }
-  }
-  __syncthreads();  // every lane has its entry state: the staging may overwrite the rows
-
-  // ---- 5. y out, pass 2, z out (each wave through its own staging slice)
-  float* stage = smem + w * staging_floats(kGenTS);
-  if (a.y) {
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-    g5_store(stage, y, lane, w, ry, m0);
-  }
-  pin(y);
-  pass2_cascade<kGenTS>(a, mt, y, m);
-  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
-      a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-  int lane_z = lane;
-  asm volatile("" : "+v"(lane_z));
-  g5_store(stage, y, lane_z, w, rz, m0);
-}
-
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
 typedef TileGeo<3, 2, 41, 0> Geo3241;
 
 struct TilePlan {
-  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen, 3: k_chain_gct<160, 147>, 4: k_chain_g5<160, 147>
+  int kind;  // 1: k_chain_tile<Geo3241>, 2: k_chain_gen, 3: k_chain_gct<160, 147>
   int64_t tsub, tile, ntiles;
   int win;   // kind 2: floats of a wave's x window
 };
@@ -1550,18 +968,6 @@ int gen_classes(int L, int M) {
 }
 constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
 
-// x window of a k_chain_g5 tile (as gen_window for 10240 outputs, +4 for the
-// shifted class rows' reach) and the kernel's LDS: the window, later the scan
-// rows, later the five staging slices.
-int g5_window(int L, int M, int T) {
-  const int64_t w = ((int64_t)(kG5Tile - 1) * M) / L + T + 4 + (kGenTT - T) + 2 + 4;
-  return (int)((w + 3) / 4 * 4);
-}
-
-size_t g5_lds_bytes(int win) {
-  return (size_t)std::max(win, std::max(kG5ScanFloats, kG5StageFloats)) * sizeof(float);
-}
-
 size_t ct_lds_bytes(int classes, int win) {
   return ((size_t)classes * kCtClassStride + (size_t)kGenWaves * win) * sizeof(float);
 }
@@ -1582,17 +988,6 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
     tp->ntiles = ceil_div(n_out, tp->tile);
     tp->win = 0;
     return true;
-  }
-  if (DSP_C5_G5 && L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) == kG5Waves) {
-    const int win = g5_window(L, M, TT);
-    if (g5_lds_bytes(win) <= kGenLdsMax) {
-      tp->kind = 4;
-      tp->tsub = kGenTS;
-      tp->tile = kG5Tile;
-      tp->ntiles = ceil_div(n_out, tp->tile);
-      tp->win = win;
-      return true;
-    }
   }
   if (L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
     // Window pairs up to (31 M div L) rounded to even + 10 past the lane's
@@ -1889,46 +1284,6 @@ void tap_pairs(const float* taps, int K, TileTables* tt) {
       }
 }
 
-template <class GEO>
-constexpr bool mfma_rows_fit() {
-  for (int i = 0; i < GEO::TSUB; ++i)
-    if (GEO::qs(i) < 8 * (i / 16) || GEO::qs(i) + 2 * GEO::NP > 8 * (i / 16) + 64) return false;
-  return true;
-}
-
-// A operands of the matrix-core SRC (TileTables::Hmf, file comment of the
-// DSP_SRC_MFMA kernel) from the tap pairs: H[i][qs(i) + 2p + e] = TP[p][phi(i)][e],
-// scaled by 2^hexp (max|H| in [2^14, 2^15)) and split into float16 hi + lo.
-template <class GEO>
-void mfma_taps(TileTables* tt) {
-  constexpr int KW = 80;  // window offsets k0(2) + 64
-  static_assert(GEO::TSUB == 48 && GEO::W <= KW, "three 16-row tiles over 80 window samples");
-  static_assert(mfma_rows_fit<GEO>(), "every row of tile m reads window offsets [8 m, 8 m + 64)");
-  std::vector<double> H((size_t)GEO::TSUB * KW, 0.0);
-  double mx = 0.0;
-  for (int i = 0; i < GEO::TSUB; ++i)
-    for (int p = 0; p < GEO::NP; ++p)
-      for (int e = 0; e < 2; ++e) {
-        const double v = tt->TP[p][GEO::phi(i)][e];
-        H[(size_t)i * KW + GEO::qs(i) + 2 * p + e] = v;
-        mx = std::max(mx, std::fabs(v));
-      }
-  int ex = 0;
-  if (mx > 0.0) std::frexp(mx, &ex);  // mx in [2^(ex-1), 2^ex)
-  tt->hexp = 15 - ex;
-  for (int m = 0; m < 3; ++m) {
-    for (int ks = 0; ks < 2; ++ks)
-      for (int lane = 0; lane < kWave; ++lane)
-        for (int j = 0; j < 8; ++j) {
-          const int row = 16 * m + (lane & 15), col = 8 * m + 32 * ks + 8 * (lane >> 4) + j;
-          const double h = std::ldexp(H[(size_t)row * KW + col], tt->hexp);
-          const _Float16 hi = (_Float16)h;
-          tt->Hmf[m][ks][0][lane][j] = hi;
-          tt->Hmf[m][ks][1][lane][j] = (_Float16)(h - (double)hi);
-        }
-  }
-}
-
 // Class tables of the generic kernel (TileTables::seq / adv).
 void gen_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables* tt) {
   const int T = (K + L - 1) / L, C = gen_classes(L, M);
@@ -1971,12 +1326,9 @@ void ct_sequences(const float* taps, int K, int L, int M, int64_t c, TileTables*
 
 // Branch 0 of the L3/M2 tile a pure delay (src_part's DLY): its tap pairs are
 // zero except the centre tap's slot, which is finite and non-zero.
-#ifndef DSP_NO_DLY
-#define DSP_NO_DLY 0  // 1: never take the DLY kernel (A/B builds)
-#endif
 template <class GEO>
 bool delay_branch(const TileTables* tt) {
-  if (DSP_NO_DLY || branch_parity<GEO>(0) < 0) return false;
+  if (branch_parity<GEO>(0) < 0) return false;
   constexpr int sl = dly_slot<GEO>();
   for (int p = 0; p < GEO::NP; ++p)
     for (int e = 0; e < 2; ++e) {
@@ -2042,10 +1394,9 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   bool dly = false;
   if (tp.kind == 1) {
     tap_pairs<Geo3241>(taps, K, tt);
-    mfma_taps<Geo3241>(tt);
     dly = delay_branch<Geo3241>(tt);
   } else gen_sequences(taps, K, L, M, c, tt);
-  if (tp.kind == 3 || tp.kind == 4) ct_sequences(taps, K, L, M, c, tt);
+  if (tp.kind == 3) ct_sequences(taps, K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
     tt->cf[k][0] = p.c[k][1];
@@ -2119,17 +1470,11 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     TraceScope trace("chain_tile", s);
     auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s, a);
-  } else if (tp.kind == 4) {
-    const size_t shm = g5_lds_bytes(tp.win);
-    auto kern = k_chain_g5<160, 147>;
-    if (int rc = allow_lds(kern, shm)) return rc;
-    TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave * kG5Waves), shm, s, a);
   } else if (tp.kind == 3) {
     const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
     const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
-    auto kern = (DSP_GCT_T7 && a.T <= 7) ? k_chain_gct<160, 147, true> : k_chain_gct<160, 147, false>;
+    auto kern = a.T <= 7 ? k_chain_gct<160, 147, true> : k_chain_gct<160, 147, false>;
     if (int rc = allow_lds(kern, shm)) return rc;
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)),

@@ -90,34 +90,21 @@ __device__ __forceinline__ pf2 vsub_mi(pf2 t, pf2 d) {
 
 
 // Variable-twiddle products and the radix-4 butterfly through the packed
-// helpers above (-DDSP_FFT_ASM=0: the float2 expressions).
-#ifndef DSP_FFT_ASM
-#define DSP_FFT_ASM 1
-#endif
+// helpers above (the float2 expressions made the compiler build each swapped,
+// negated twiddle copy with a move and an xor).
 __device__ __forceinline__ float2 cmulv(float2 a, float2 w) {
-#if DSP_FFT_ASM
   const pf2 r = vcmul(pf2{a.x, a.y}, pf2{w.x, w.y});
   return make_float2(r.x, r.y);
-#else
-  return cmul(a, w);
-#endif
 }
 
 // |v|.  sqrtf is correctly rounded, which the compiler expands around
 // v_sqrt_f32 into ~14 instructions (denormal scaling and a two-sided fma
 // correction); the bare instruction is within 1 ulp, 2^-23 relative, far inside
 // the spectra's 1e-5 tolerance, and drops ~450 of the ~2900 VALU instructions
-// a 4096-point magnitude spectrum takes per wave.  -DDSP_MAG_CR=1: sqrtf.
-#ifndef DSP_MAG_CR
-#define DSP_MAG_CR 0
-#endif
+// a 4096-point magnitude spectrum takes per wave.
 __device__ __forceinline__ float cabsf_(float2 v) {
   const float p = fmaf(v.x, v.x, v.y * v.y);
-#if DSP_MAG_CR
-  return sqrtf(p);
-#else
   return __builtin_amdgcn_sqrtf(p);
-#endif
 }
 
 // a * W_16^q for a compile-time q (after unrolling); exact for q % 4 == 0.
@@ -150,16 +137,10 @@ __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2&
   const float2 t2 = cadd(a1, a3), d = csub(a1, a3);
   a0 = cadd(t0, t2);
   a2 = csub(t0, t2);
-#if DSP_FFT_ASM
   const pf2 r1 = vadd_mi(pf2{t1.x, t1.y}, pf2{d.x, d.y});  // t1 + (a1 - a3) * (-i)
   const pf2 r3 = vsub_mi(pf2{t1.x, t1.y}, pf2{d.x, d.y});
   a1 = make_float2(r1.x, r1.y);
   a3 = make_float2(r3.x, r3.y);
-#else
-  const float2 t3 = make_float2(d.y, -d.x);  // (a1 - a3) * (-i)
-  a1 = cadd(t1, t3);
-  a3 = csub(t1, t3);
-#endif
 }
 
 // In-place forward DFT of R points, natural order in and out.
@@ -545,18 +526,11 @@ __device__ __forceinline__ void spec_stream_load(const FftArgs& a, const InRow& 
       raw[q][r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 4 * 2 * (2 * q + r * SS::S0), 2);
 }
 
-#ifndef DSP_SPEC_WAVES
-#define DSP_SPEC_WAVES 3   // waves per SIMD the streaming kernel is compiled for
-#endif
-#ifndef DSP_SPEC_TPBX
-#define DSP_SPEC_TPBX 2    // transforms per workgroup (1: same at 32768 ch, 8 % slower at 4096)
-#endif
-#ifndef DSP_SPEC_LOWREG
-#define DSP_SPEC_LOWREG 1  // twiddle powers by squaring (few live VGPRs)
-#endif
+constexpr int kSpecWaves = 3;  // waves per SIMD the streaming kernel is compiled for
+constexpr int kSpecTpbx = 2;   // transforms per workgroup (1: same at 32768 ch, 8 % slower at 4096)
 template <int LOG2N, int TPBX>
 __global__ __launch_bounds__(TPBX * Plan<LOG2N - 1>::TPT)
-__attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs a, int64_t units) {
+__attribute__((amdgpu_waves_per_eu(kSpecWaves))) void k_spec_stream(FftArgs a, int64_t units) {
   using SS = SpecStream<LOG2N>;
   using PL = typename SS::PL;
   constexpr int NH = SS::NH, R0 = SS::R0, NB0 = SS::NB0, NQ = SS::NQ;
@@ -622,7 +596,7 @@ __attribute__((amdgpu_waves_per_eu(DSP_SPEC_WAVES))) void k_spec_stream(FftArgs 
     }
     __syncthreads();
     if constexpr (PL::NP > 1)
-      run_pass<LOG2N - 1, 1, LdsIO<NH>, DSP_SPEC_LOWREG>(LdsIO<NH>{buf}, buf, jj, tw);
+      run_pass<LOG2N - 1, 1, LdsIO<NH>, true>(LdsIO<NH>{buf}, buf, jj, tw);
     __syncthreads();  // the last pass stored Z into LDS
     if (live) {
       float* mr = a.out + t * a.ld_out;
@@ -667,7 +641,7 @@ int resident_groups(int threads, size_t shm) {
 template <int LOG2N>
 int launch_spec_stream(const FftArgs& a, hipStream_t s) {
   using PL = Plan<LOG2N - 1>;
-  constexpr int TPBX = DSP_SPEC_TPBX;
+  constexpr int TPBX = kSpecTpbx;
   const size_t shm = (size_t)TPBX * PL::PADN * sizeof(float2);
   if (int rc = allow_lds(k_spec_stream<LOG2N, TPBX>, shm)) return rc;
   const int64_t units = ceil_div(a.B, TPBX);
@@ -682,7 +656,7 @@ int launch_spec_stream(const FftArgs& a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // One-wave 4096-point magnitude spectrum (round 3; the default for log2n = 12,
-// the benchmark's n_fft; -DDSP_SPEC_WAVE=0 keeps k_spec_stream).  A wave owns
+// the benchmark's n_fft).  A wave owns
 // one transform at a time and never waits on another wave: the 2048 packed
 // values c[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] sit 32 per lane and the
 // 2048-point transform is a 32 x 64 four-step split
@@ -710,21 +684,9 @@ __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t
   return m < N / 2 ? w : make_float2(-w.x, -w.y);
 }
 
-#ifndef DSP_SPEC_WAVE
-#define DSP_SPEC_WAVE 1
-#endif
-#ifndef DSP_SPEC_WAVE_PF
-#define DSP_SPEC_WAVE_PF 0  // 1: prefetch the next frame in 64 VGPRs (2 waves per SIMD)
-#endif
 constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
 constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
-#ifndef DSP_SPEC_WPG
-#define DSP_SPEC_WPG 4
-#endif
-#ifndef DSP_SPEC_WPE
-#define DSP_SPEC_WPE 3
-#endif
-constexpr int kWavePerGroup = DSP_SPEC_WPG;
+constexpr int kWavePerGroup = 4;
 
 // W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).  oz: an
 // opaque zero OR-ed into the bits, so that the constants are formed where they
@@ -837,12 +799,11 @@ __device__ __forceinline__ void wave_frame_load(const FftArgs& a, int64_t t, int
     raw[n1] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * lane, 512 * n1, 2);
 }
 
-// PF = 1: the next frame's samples load into 64 more VGPRs while this one
-// computes (226 VGPRs, 2 waves per SIMD); PF = 0: no prefetch, 149 VGPRs and 3
-// waves per SIMD.  Same arithmetic, same bits.
-template <int PF>
+// No prefetch of the next frame: 149 VGPRs and 3 waves per SIMD.  (Holding
+// the next frame in 64 more VGPRs, 2 waves per SIMD, measured 0.199 vs 0.194
+// ms at config 4, profiles/r03_spec_wave_oz_ab.jsonl.)
 __global__ __launch_bounds__(64 * kWavePerGroup)
-__attribute__((amdgpu_waves_per_eu(PF ? 2 : DSP_SPEC_WPE))) void k_spec_wave12(FftArgs a) {
+__attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
   constexpr int N = 4096, NH = 2048;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   const int lane = threadIdx.x & 63;
@@ -861,11 +822,9 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : DSP_SPEC_WPE))) void k_spec_wave12(F
   const float sg = hi ? -1.f : 1.f;
   const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
   int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv;
-  // the frame in flight: transform t + nw's samples load while t computes
   u32x2_t raw[32];
-  if (PF && t < a.B) wave_frame_load(a, t, lane, raw);
   for (; t < a.B; t += nw) {
-    if (!PF) wave_frame_load(a, t, lane, raw);
+    wave_frame_load(a, t, lane, raw);
     // an opaque per-iteration copy of the lane's parity: the combine's 31
     // per-lane twiddles below are loop-invariant, and hoisting them would
     // hold 62 VGPRs
@@ -895,7 +854,6 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : DSP_SPEC_WPE))) void k_spec_wave12(F
       v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} *
               win[64 * n1 + lane];
     }
-    if (PF && t + nw < a.B) wave_frame_load(a, t + nw, lane, raw);
     // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
     // powers come from the table every 8 steps and by products in between)
     pdft32(v, z0);
@@ -955,26 +913,16 @@ __attribute__((amdgpu_waves_per_eu(PF ? 2 : DSP_SPEC_WPE))) void k_spec_wave12(F
   }
 }
 
-template <int PF>
-int launch_spec_wave12_pf(const FftArgs& a, hipStream_t s, size_t shm, int res) {
+int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
+  if (int rc = allow_lds(k_spec_wave12, shm)) return rc;
+  const int res = resident_groups<k_spec_wave12>(64 * kWavePerGroup, shm);
+  DSP_REQUIRE(res > 0, "occupancy query failed");
   const int64_t groups = ceil_div(a.B, kWavePerGroup);
   const unsigned grid = (unsigned)(groups < res ? groups : res);
-  hipLaunchKernelGGL(k_spec_wave12<PF>, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
+  hipLaunchKernelGGL(k_spec_wave12, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
   DSP_LAUNCHED("k_spec_wave12");
   return DSP_OK;
-}
-
-// PF = 0 since the opaque-zero constants (w128) cut its VALU by 12 %: 0.194 vs
-// 0.199 ms (PF = 1) at config 4, 0.052 vs 0.056 at config 5
-// (profiles/r03_spec_wave_oz_ab.jsonl); with the hoisted constants PF = 1 had
-// won at config 4 (profiles/r03_spec_wave_pf_ab.jsonl).
-int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
-  constexpr int PF = DSP_SPEC_WAVE_PF;
-  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
-  if (int rc = allow_lds(k_spec_wave12<PF>, shm)) return rc;
-  const int res = resident_groups<k_spec_wave12<PF>>(64 * kWavePerGroup, shm);
-  DSP_REQUIRE(res > 0, "occupancy query failed");
-  return launch_spec_wave12_pf<PF>(a, s, shm, res);
 }
 
 // ---------------------------------------------------------------------------
@@ -1111,18 +1059,16 @@ template <int MODE>
 int dispatch(const FftArgs& a, int log2n, hipStream_t s);
 
 int dispatch_spec(const FftArgs& a, int log2n, hipStream_t s) {
-#if !DSP_SPEC_V1
   switch (log2n) {  // sizes whose first pass has radix < 16: the streaming kernel
     case 6: return launch_spec_stream<6>(a, s);
     case 7: return launch_spec_stream<7>(a, s);
     case 8: return launch_spec_stream<8>(a, s);
     case 10: return launch_spec_stream<10>(a, s);
     case 11: return launch_spec_stream<11>(a, s);
-    case 12: return DSP_SPEC_WAVE ? launch_spec_wave12(a, s) : launch_spec_stream<12>(a, s);
+    case 12: return launch_spec_wave12(a, s);
     case 14: return launch_spec_stream<14>(a, s);
     default: break;
   }
-#endif
   switch (log2n) {
     case 5: return launch_spec_real<5>(a, s);
     case 6: return launch_spec_real<6>(a, s);

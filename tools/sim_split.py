@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Accuracy model of the matrix-core SRC variant (-DDSP_SRC_MFMA=1,
+"""Accuracy model of the matrix-core SRC variant (measured in round 3 and removed;
 csrc/chain_tile.hip): config 3's SRC (L3/M2, K121) computed as float32 FMAs
 (the default kernel), as float16 hi + lo operand splits with four products
 (x and taps scaled by powers of two) and as bfloat16 three-way splits with six
