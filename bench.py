@@ -132,12 +132,13 @@ def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
     then settles over the first ~20-40 ms of a busy GPU: a 1 ms config-3 step
     measured 0.86 -> 1.19 -> 0.89 ms over its first 20 launches), then W untimed
     warmup steps, then K steps bracketed by barrier + sync on both sides.
-    Returns the elapsed seconds, maxed over ranks when `dist` is initialised
-    (a gloo group: the max is a CPU all-reduce).  Each rank's clock runs from
-    the start barrier to its own final sync: the end barrier still holds every
-    rank until the slowest is done, but its gloo round trips (a sizeable share
-    of a ~17 ms N = 8 timed region) stay out of the time; the max over ranks is
-    the job's time."""
+    Returns the elapsed seconds; with `dist` initialised (a gloo group) the
+    job's time over all ranks, max(end) - min(start) on the host's monotonic
+    clock (perf_counter is CLOCK_MONOTONIC, one clock for every process of the
+    node): each rank stamps its start as it leaves the start barrier and its
+    end at its own final sync, so skew in leaving the barrier counts, and the
+    end barrier's gloo round trips (a sizeable share of a ~17 ms N = 8 timed
+    region) do not."""
     t_pre = time.perf_counter()
     while preheat_s > 0:
         step()
@@ -157,11 +158,12 @@ def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
     elapsed = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t_end = torch.tensor([t0 + elapsed], dtype=torch.float64)
+        t_start = torch.tensor([t0], dtype=torch.float64)
+        dist.all_reduce(t_end, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_start, op=dist.ReduceOp.MIN)
+        elapsed = float(t_end.item() - t_start.item())
     return elapsed
 
 

@@ -70,7 +70,10 @@ int dsp_version(void) {
   // dsp_chain_tile_tables returns the key; the chain workspace holds the
   // single-pass region and the cascade's scratch side by side;
   // dsp_chain_status / dsp_chain_spin_limit added (round 3).
-  return 20000;
+  // 2.1.0: every SRC entry point takes the caller's float32 taps and flushes
+  // the sinc-zero noise itself (common.h, kTapFlushRel); inf and NaN input
+  // propagate as through the reference's float64 convolution (round 4).
+  return 20100;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }

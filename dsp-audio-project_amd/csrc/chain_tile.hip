@@ -187,6 +187,9 @@ struct TileTables {
   // shift s_i = (i M div L) mod 2 + (1 if the class's phase carries q one
   // further, else 0), zero outside the T taps.
   alignas(16) float seqs[kGenClasses][kGenTS][kCtRow];
+  // Largest flushed |tap| (common.h, kTapFlushRel), for the non-finite path.
+  float flush_thr;
+  int32_t pad3[3];
 };
 
 struct TileArgs {
@@ -207,6 +210,12 @@ struct TileArgs {
 };
 
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
+
+// The lane's index in its wave, recomputed (mbcnt): late uses of threadIdx.x
+// would keep its VGPR live through the whole kernel.
+__device__ __forceinline__ int lane_id() {
+  return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
 
 // Pins v[0..N) at this point of the program: the values are computed before it
 // and later uses start after it.  Keeps the scheduler from overlapping phases
@@ -395,6 +404,8 @@ __device__ __forceinline__ void tile_entry_state(const TileArgs& a, int64_t b, i
 // LDS floats store_tile<TS> stages through.
 __host__ __device__ constexpr int staging_floats(int ts) { return (kWave / 2) * (ts + 4); }
 
+__device__ __forceinline__ void pass1_basis(tt_ptr mt, const f32x2 (&e2)[kD], double (&v)[kD]);
+
 // Pass 1 (file comment, step 2): the sub-chunk's zero-state end state in
 // block-diagonal coordinates, E' = Q sum_i Gc[i] y[i] (float32 sums in
 // input-normal coordinates, one float64 change of basis).
@@ -420,6 +431,13 @@ __device__ __forceinline__ void pass1_state(tt_ptr mt, const float (&y)[TS], dou
         e2[d] = __builtin_elementwise_fma(f32x2{tq->Gc[j][d][0], tq->Gc[j][d][1]}, u, e2[d]);
     }
     pin(e2);
+    pass1_basis(mt, e2, v);
+  }
+}
+
+// Pass 1's change of basis: E' = Q e in float64, e = the input-normal sums.
+__device__ __forceinline__ void pass1_basis(tt_ptr mt, const f32x2 (&e2)[kD], double (&v)[kD]) {
+  {
     f32x2 e[kS];
 #pragma unroll
     for (int k = 0; k < kS; ++k)
@@ -489,16 +507,91 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
   }
 }
 
+// Rare path of a tile with non-finite input (tile_cascade): every output of
+// the lane through window_sums / nf_fix (sums(i, nf, fin) gives output i's),
+// then the lane's E': NaN if its y holds an inf or NaN, else pass 1 rerun on
+// the fixed y (a zero tap's NaN may have been all there was).  The outputs
+// wait in the tile's own z outputs (z0: output 0 of the lane; pass 2
+// overwrites them), and the loops over them are rolled: unrolled over
+// registers or staged in a private array, this code cost the hot path
+// registers (VGPR and SGPR spills, the scratch setup's SGPRs).
+template <int TS, class SUMS>
+__device__ __forceinline__ void fix_outputs(const TileArgs& a, tt_ptr mt, int64_t b, int64_t z0,
+                                            float (&y)[TS], double (&v)[kD], SUMS&& sums) {
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+      a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+  const int off0 = (int)(z0 * 4);  // outputs past n_out: dropped / read as 0, never stored
+  auto get = [&](int i) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, off0 + 4 * i, 0, 1));
+  };
+  auto put = [&](int i, float f) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f), rz, off0 + 4 * i, 0, 0);
+  };
+#pragma unroll
+  for (int i = 0; i < TS; ++i) put(i, y[i]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bool any = false;
+#pragma unroll 1
+  for (int i = 0; i < TS; ++i) {
+    float nf, fin, f = get(i);
+    sums(i, nf, fin);
+    any |= nf_fix(f, nf, fin);
+    put(i, f);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (any) {
+#pragma unroll
+    for (int d = 0; d < kD; ++d) v[d] = __builtin_nan("");
+  } else {
+    // pass1_state's sums in its order (bitwise the same E'), rolled
+    f32x2 e2[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) e2[d] = f32x2{0.f, 0.f};
+#pragma unroll 1
+    for (int j = 0; j < TS / 2; ++j) {
+      const f32x2 u = f32x2{get(2 * j), get(2 * j + 1)};
+#pragma unroll
+      for (int d = 0; d < kD; ++d)
+        e2[d] = __builtin_elementwise_fma(f32x2{mt->Gc[j][d][0], mt->Gc[j][d][1]}, u, e2[d]);
+    }
+    pass1_basis(mt, e2, v);
+  }
+#pragma unroll
+  for (int i = 0; i < TS; ++i) y[i] = get(i);
+}
+
 // Steps 2-5 of the tile (file comment) for a wave that holds its y sub-chunk:
 // pass 1, entry state (hand-off) and scan, publish, y out, s = T m, pass 2,
-// z out.  lds: at least staging_floats(TS) floats the wave may overwrite.
-template <int TS, bool YST = true>
+// z out.  lds: at least staging_floats(TS) floats the wave may overwrite; the
+// x window there stays intact until pass 1 is done.
+//
+// Non-finite input.  Every x sample of a lane's window meets an FMA of some
+// output of the lane whose polyphase branch is not the pure delay (flushed
+// taps included: 0 * inf = NaN), so a window holding an inf or NaN leaves a
+// non-finite y, E' and (fma by any finite coefficient keeps it non-finite)
+// end state of the tile, and of every later tile of the channel.  The
+// single-pass kernels do nothing about it; every tile publishes its end state,
+// the channel's last one included, and the repair kernel that follows them
+// (k_chain_*_repair) reruns a channel whose last end state is not finite from
+// its first tile with a non-finite end state on.  There REPAIR tiles whose
+// pass-1 state is not finite (one class test per lane, a wave ballot) call
+// on_nf(y, v), which recomputes y with the reference's non-finite semantics
+// (fix_outputs: window_sums / nf_fix; finite windows keep the canonical sums,
+// recomputed from the window with its infs and NaNs zeroed, since the packed
+// FMAs of a neighbouring output may have picked one up through a zero tap),
+// reruns pass 1 on the fixed y and makes E' NaN for a lane whose y holds an
+// inf or NaN (as nf_poison: every later output of the channel is NaN, as in
+// the reference's cascade).
+template <int TS, bool YST = true, bool REPAIR = false, class ONNF>
 __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
                                              float (&y)[TS], int lane, int64_t b, int64_t tile,
-                                             int64_t m0) {
+                                             int64_t m0, ONNF&& on_nf) {
   // ---- 2. pass 1: zero-state end state of the sub-chunk
   double v[kD];
   pass1_state<TS>(mt, y, v);
+  if constexpr (REPAIR) {
+    if (__builtin_amdgcn_ballot_w64(!__builtin_isfinite(v[kD - 1]))) on_nf(y, v);  // wave-uniform
+  }
   // Keep the SRC and pass 1 ahead of the hand-off wait (the compiler would
   // otherwise sink them past it).
   pin(v);
@@ -598,15 +691,18 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     u1 = n1;
     if (worker) *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * kb) = f64x2{u0, u1};
   }
-  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)
-  if (tile + 1 < a.ntiles) {
+  // ---- 4. publish the tile's end state (segment 7's workers hold v_63); the
+  // channel's last tile too, for the repair kernel (no flag: nobody waits)
+  {
     const int64_t me = b * a.ntiles + tile;
     if (worker && sg == 7) {
       store_state(a.states + me * kD + 2 * kb, u0);
       store_state(a.states + me * kD + 2 * kb + 1, u1);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 8 * 7) store_flag(a.flags + me, 1u);
+    if (tile + 1 < a.ntiles) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 8 * 7) store_flag(a.flags + me, 1u);
+    }
   }
   fence();
   double m[kD];
@@ -637,16 +733,65 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   store_tile<TS>(lds, y, lane_z, rz, m0);
 }
 
-template <class GEO, bool DLY = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
-    TileArgs a) {
+// Repair kernels (k_chain_*_repair), launched after every single-pass kernel
+// on its stream.  Each wave reads the last end state of 64 channels at a time
+// (B * 8 bytes for the whole launch: a clean launch costs a few microseconds)
+// and reruns every channel whose state is not finite (repair_channel).
+// A channel's tiles run in order from its first tile with a non-finite end
+// state: the tile before it is clean and its published end state is the entry
+// state; later ones take this loop's own, through the hand-off protocol itself
+// (the flag is raised here, consumed and cleared by tile_entry_state, and
+// the flag a rerun tile raised is cleared after it).  A rerun of a tile whose
+// window is clean gives the single-pass kernel's y and z bitwise, so every
+// tile from the first non-finite end state on is rerun: which of them are
+// wrong (a NaN through a zero tap of a neighbouring output, a delay output
+// that skipped its window) is not recorded anywhere.
+template <class BODY>
+__device__ __forceinline__ void repair_channel(const TileArgs& a, int lane, int64_t b,
+                                               BODY&& body) {
+  const double* st = a.states + b * a.ntiles * kD + (kD - 1);
+  uint32_t* fl = a.flags + b * a.ntiles;
+  int64_t first = a.ntiles;
+  for (int64_t t0 = 0; t0 < a.ntiles && first == a.ntiles; t0 += kWave) {
+    const int64_t t = t0 + lane;
+    const uint64_t bad =
+        __builtin_amdgcn_ballot_w64(t < a.ntiles && !__builtin_isfinite(st[t * kD]));
+    if (bad) first = t0 + __builtin_ctzll(bad);
+  }
+  for (int64_t tile = first; tile < a.ntiles; ++tile) {
+    if (lane == 0 && tile > 0) store_flag(fl + tile - 1, 1u);  // states[tile - 1]: the entry
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    body(tile);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) store_flag(fl + tile, 0u);  // no flag left raised for the next call
+  }
+}
+
+// The repair kernels' channel loop: wave `wave` of `waves` per workgroup.
+template <class BODY>
+__device__ __forceinline__ void repair_channels(const TileArgs& a, int wave, int waves,
+                                                BODY&& body) {
+  const int lane = lane_id();
+  const int64_t stride = (int64_t)gridDim.x * waves * kWave;
+  for (int64_t b0 = ((int64_t)blockIdx.x * waves + wave) * kWave; b0 < a.B; b0 += stride) {
+    const int64_t b = b0 + lane;
+    const double last = b < a.B ? a.states[(b * a.ntiles + a.ntiles - 1) * kD + (kD - 1)] : 0.0;
+    uint64_t bad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(last));
+    while (bad) {
+      const int64_t bb = b0 + __builtin_ctzll(bad);
+      bad &= bad - 1;
+      repair_channel(a, lane, bb, [&](int64_t tile) { body(bb, tile); });
+    }
+  }
+}
+
+// One tile of the L3/M2 kernel (REPAIR: the rerun with the non-finite path).
+template <class GEO, bool DLY, bool REPAIR>
+__device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, int lane, int64_t b,
+                                                int64_t tile) {
   constexpr int TS = GEO::TSUB;
-  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
-  const int lane = threadIdx.x;
-  const int64_t id = blockIdx.x;
-  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
-  const int64_t m0 = tile * GEO::TILE;                 // first output of the tile
-  const tt_ptr mt = (tt_ptr)a.tt;  // wave-uniform: scalar loads
+  const int64_t m0 = tile * GEO::TILE;  // first output of the tile
+  const tt_ptr mt = (tt_ptr)a.tt;       // wave-uniform: scalar loads
 
   // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
   {
@@ -683,7 +828,39 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
       pin(y);
     }
   }
-  tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0);
+  if constexpr (REPAIR) {
+    // each output's reference sums over its window (window_sums, nf_fix)
+    auto fix = [&](float (&yy)[TS], double (&v)[kD]) {
+      const float thr = mt->flush_thr;
+      fix_outputs(a, mt, b, m0 + TS * lane, yy, v, [&](int i, float& nf, float& fin) {
+        const int j = i * GEO::M + GEO::CR;
+        const int base = kLS * lane + j / GEO::L + GEO::TT - 1;  // window offset of x[q]
+        // (window starts and q keep x's absolute parity: xs0 is a multiple of 4)
+        window_sums(a.taps, a.K, GEO::L, j % GEO::L, thr, base,
+                    [&](int t) { return lds[xpad(base - t)]; }, nf, fin);
+      });
+    };
+    tile_cascade<TS, true, true>(a, mt, lds, y, lane, b, tile, m0, fix);
+  } else {
+    tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0);
+  }
+}
+
+template <class GEO, bool DLY = false>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
+    TileArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  const int64_t id = blockIdx.x;
+  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
+  chain_tile_body<GEO, DLY, false>(a, lds, threadIdx.x, b, tile);
+}
+
+template <class GEO, bool DLY = false>
+__global__ __launch_bounds__(kWave) void k_chain_tile_repair(TileArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  repair_channels(a, 0, 1, [&](int64_t b, int64_t tile) {
+    chain_tile_body<GEO, DLY, true>(a, lds, (int)threadIdx.x, b, tile);
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -704,65 +881,84 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 // Each wave owns its x window (and stages its stores through it).  Steps 2-5
 // are tile_cascade<32>.
 // ---------------------------------------------------------------------------
-template <bool UP>
-__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
-k_chain_gen(TileArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
-  const int64_t tile = blockIdx.x / groups;
-  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+// The generic kernels' workgroup: kGenWaves waves, wave w takes channel
+// g kGenWaves + w of channel group g; the ids are tile-major over groups.
+__device__ __forceinline__ int gen_wave() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+}
+
+// Tile x window of a generic kernel's wave: x[qa .. qa + a.win) (zeros
+// outside [0, n_in)), 8 float4 loads in flight per lane per round.
+__device__ __forceinline__ void gen_load_window(const TileArgs& a, float* win, int lane, int64_t b,
+                                                int64_t qa) {
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+  const int nf = a.win >> 2;
+  for (int f0 = 0; f0 < nf; f0 += 8 * kWave) {
+    f32x4 v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int f = f0 + r * kWave + lane;  // past the window: harmless reads
+      v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int f = f0 + r * kWave + lane;
+      if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+    }
+  }
+}
+
+// Class tables of k_chain_gen into LDS (class stride kGenClassStride floats:
+// the rows that lanes of different classes read together start on distinct
+// bank quads), then the advance masks; two float4 loads in flight per thread.
+// Ends with a workgroup barrier.
+__device__ __forceinline__ void gen_load_classes(const TileArgs& a, float* seq, uint32_t* adv) {
+  constexpr int kNT = kWave * kGenWaves;
+  constexpr int kF4 = kGenTS * kGenTT / 4;  // float4s per class
+  const int C = ((tt_ptr)a.tt)->classes;
+  const f32x4* src = reinterpret_cast<const f32x4*>(a.tt->seq);
+  f32x4 v[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) v[r] = src[(r * kNT + threadIdx.x) & (kGenClasses * kF4 - 1)];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int i = r * kNT + threadIdx.x, k = i / kF4, f = i - k * kF4;
+    if (k < C) *reinterpret_cast<f32x4*>(seq + k * kGenClassStride + 4 * f) = v[r];
+  }
+  if (threadIdx.x < kGenClasses) adv[threadIdx.x] = a.tt->adv[threadIdx.x];
+  __syncthreads();
+}
+
+// The generic kernels' on_nf for the repair rerun: window x[qa ..] unpadded
+// in `win`, the lane's outputs m0 + 32 lane + i with j0 = (m0 + 32 lane) M + c.
+__device__ __forceinline__ void gen_fix(const TileArgs& a, tt_ptr mt, const float* win, int64_t qa,
+                                        int64_t j0, int64_t b, int64_t z0, float (&yy)[kGenTS],
+                                        double (&v)[kD]) {
+  const float thr = mt->flush_thr;
+  fix_outputs(a, mt, b, z0, yy, v, [&](int i, float& nf, float& fin) {
+    const int64_t j = j0 + (int64_t)i * a.M, q = j / a.L;
+    const int base = (int)(q - qa);
+    window_sums(a.taps, a.K, a.L, (int)(j - q * a.L), thr, a.T - 1,
+                [&](int t) { return win[base - t]; }, nf, fin);
+  });
+}
+
+// One tile of k_chain_gen for one wave (REPAIR: the rerun with the
+// non-finite path).
+template <bool UP, bool REPAIR>
+__device__ __forceinline__ void chain_gen_body(const TileArgs& a, const float* seq,
+                                               const uint32_t* adv, float* win, int lane,
+                                               int64_t b, int64_t tile) {
   const int L = a.L, M = a.M, T = a.T;
   const tt_ptr mt = (tt_ptr)a.tt;
   const int C = mt->classes;
-  // Class tables into LDS (class stride kGenClassStride floats: the rows that
-  // lanes of different classes read together start on distinct bank quads),
-  // then the advance masks; two float4 loads in flight per thread.
-  float* seq = smem;
-  uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
-  {
-    constexpr int kNT = kWave * kGenWaves;
-    constexpr int kF4 = kGenTS * kGenTT / 4;  // float4s per class
-    const f32x4* src = reinterpret_cast<const f32x4*>(a.tt->seq);
-    f32x4 v[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) v[r] = src[(r * kNT + threadIdx.x) & (kGenClasses * kF4 - 1)];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = r * kNT + threadIdx.x, k = i / kF4, f = i - k * kF4;
-      if (k < C) *reinterpret_cast<f32x4*>(seq + k * kGenClassStride + 4 * f) = v[r];
-    }
-    if (threadIdx.x < kGenClasses) adv[threadIdx.x] = a.tt->adv[threadIdx.x];
-  }
-  __syncthreads();
-  if (b >= a.B) return;
-  float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
   const int64_t m0 = tile * kGenTile;
 
-  // ---- x window of the tile: x[qa .. qa + nload) (zeros outside [0, n_in))
+  // ---- x window of the tile
   const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
   const int64_t qa = (qlo >> 2) << 2;  // floor to a multiple of 4
-  {
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
-    // The whole window (taps past T read real samples), 8 float4 loads in
-    // flight per lane per round.
-    const int nf = a.win >> 2;
-    for (int f0 = 0; f0 < nf; f0 += 8 * kWave) {
-      f32x4 v[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kWave + lane;  // past the window: harmless reads
-        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kWave + lane;
-        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
-      }
-    }
-  }
+  gen_load_window(a, win, lane, b, qa);
   fence();
 
   // ---- 1. SRC of the lane's 32 outputs, software-pipelined one output deep
@@ -770,8 +966,8 @@ k_chain_gen(TileArgs a) {
   // q advances by 0 or 1 per output, so the 8-sample window slides in
   // registers and one new sample is read per output; otherwise all 8 are read.
   float y[kGenTS];
+  const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
   {
-    const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
     const int64_t q0 = j0 / L;
     int qr = (int)(q0 - (T - 1) - qa);  // window offset of the output's first tap
     const int dq = M / L;
@@ -826,7 +1022,44 @@ k_chain_gen(TileArgs a) {
     }
   }
   pin(y);
-  tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
+  if constexpr (REPAIR)
+    tile_cascade<kGenTS, true, true>(a, mt, win, y, lane, b, tile, m0,
+                                     [&](float (&yy)[kGenTS], double (&v)[kD]) {
+                                       gen_fix(a, mt, win, qa, j0, b, m0 + kGenTS * lane, yy, v);
+                                     });
+  else
+    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0);
+}
+
+template <bool UP>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gen(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
+  const int64_t tile = blockIdx.x / groups;
+  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  float* seq = smem;
+  uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
+  gen_load_classes(a, seq, adv);
+  if (b >= a.B) return;
+  float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
+  chain_gen_body<UP, false>(a, seq, adv, win, lane, b, tile);
+}
+
+template <bool UP>
+__global__ __launch_bounds__(kWave * kGenWaves) void k_chain_gen_repair(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  float* seq = smem;
+  uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
+  gen_load_classes(a, seq, adv);
+  float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
+  repair_channels(a, w, kGenWaves, [&](int64_t b, int64_t tile) {
+    chain_gen_body<UP, true>(a, seq, adv, win, lane, b, tile);
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -844,62 +1077,41 @@ k_chain_gen(TileArgs a) {
 // T7 (T <= 7 taps per branch, config 5's K = 1023): an output whose g_i is
 // even has shift d_i in {0, 1}, so its taps fill slots 0..7 and slots 8, 9 are
 // zero: the last tap-pair read and FMA are skipped (bitwise the same y).
-template <int L, int M, bool T7 = false>
-__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
-k_chain_gct(TileArgs a) {
+// Class rows of k_chain_gct into LDS (the C classes in use only).  Ends with
+// a workgroup barrier.
+__device__ __forceinline__ void ct_load_classes(const TileArgs& a, float* seq) {
+  constexpr int kF4 = kGenTS * kCtRow / 4;  // float4s per class
+  const int C = ((tt_ptr)a.tt)->classes;
+  const f32x4* src = reinterpret_cast<const f32x4*>(&a.tt->seqs[0][0][0]);
+  for (int i = threadIdx.x; i < C * kF4; i += kWave * kGenWaves) {
+    const int k = i / kF4, f = i - k * kF4;
+    *reinterpret_cast<f32x4*>(seq + k * kCtClassStride + 4 * f) = src[i];
+  }
+  __syncthreads();
+}
+
+// One tile of k_chain_gct for one wave (REPAIR: the rerun with the
+// non-finite path).
+template <int L, int M, bool T7, bool REPAIR>
+__device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* seq, float* win,
+                                               int lane, int64_t b, int64_t tile) {
   static_assert(M < L, "q advances by 0 or 1 per output");
   constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
-  const int64_t tile = blockIdx.x / groups;
-  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
   const int T = a.T;
   const tt_ptr mt = (tt_ptr)a.tt;
   const int C = mt->classes;
-  // Class rows into LDS (the C classes in use only).
-  float* seq = smem;
-  {
-    constexpr int kF4 = kGenTS * kCtRow / 4;  // float4s per class
-    const f32x4* src = reinterpret_cast<const f32x4*>(&a.tt->seqs[0][0][0]);
-    for (int i = threadIdx.x; i < C * kF4; i += kWave * kGenWaves) {
-      const int k = i / kF4, f = i - k * kF4;
-      *reinterpret_cast<f32x4*>(seq + k * kCtClassStride + 4 * f) = src[i];
-    }
-  }
-  __syncthreads();
-  if (b >= a.B) return;
-  float* win = smem + C * kCtClassStride + w * a.win;
   const int64_t m0 = tile * kGenTile;
 
-  // ---- x window of the tile: x[qa .. qa + win) (zeros outside [0, n_in))
+  // ---- x window of the tile
   const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
   const int64_t qa = (qlo >> 2) << 2;
-  {
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
-    const int nf = a.win >> 2;
-    for (int f0 = 0; f0 < nf; f0 += 8 * kWave) {
-      f32x4 v[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kWave + lane;  // past the window: harmless reads
-        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * f) * 4), 0, kStream);
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int f = f0 + r * kWave + lane;
-        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
-      }
-    }
-  }
+  gen_load_window(a, win, lane, b, qa);
   fence();
 
   // ---- 1. SRC of the lane's 32 outputs from its register window
   float y[kGenTS];
+  const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
   {
-    const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
     const float* xl = win + (int)(j0 / L - (T - 1) - qa);
     const float* row = seq + (int)((tile * kWave + lane) % C) * kCtClassStride;
     f32x2 X[NPW];
@@ -924,9 +1136,43 @@ k_chain_gct(TileArgs a) {
     }
   }
   pin(y);
-  tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0);
+  if constexpr (REPAIR)
+    tile_cascade<kGenTS, true, true>(a, mt, win, y, lane, b, tile, m0,
+                                     [&](float (&yy)[kGenTS], double (&v)[kD]) {
+                                       gen_fix(a, mt, win, qa, j0, b, m0 + kGenTS * lane, yy, v);
+                                     });
+  else
+    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0);
 }
 
+template <int L, int M, bool T7 = false>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gct(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
+  const int64_t tile = blockIdx.x / groups;
+  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  float* seq = smem;
+  ct_load_classes(a, seq);
+  if (b >= a.B) return;
+  float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
+  chain_gct_body<L, M, T7, false>(a, seq, win, lane, b, tile);
+}
+
+template <int L, int M, bool T7 = false>
+__global__ __launch_bounds__(kWave * kGenWaves) void k_chain_gct_repair(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  float* seq = smem;
+  ct_load_classes(a, seq);
+  float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
+  repair_channels(a, w, kGenWaves, [&](int64_t b, int64_t tile) {
+    chain_gct_body<L, M, T7, true>(a, seq, win, lane, b, tile);
+  });
+}
 
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
@@ -967,6 +1213,7 @@ int gen_classes(int L, int M) {
   return (int)(L / gcd64(((int64_t)kGenTS * M) % L, L));
 }
 constexpr size_t kGenLdsMax = 64 * 1024;  // two workgroups (8 waves) per CU at least
+constexpr int64_t kRepairGroups = 1024;     // workgroups of a repair kernel
 
 size_t ct_lds_bytes(int classes, int win) {
   return ((size_t)classes * kCtClassStride + (size_t)kGenWaves * win) * sizeof(float);
@@ -1391,12 +1638,18 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
   TileTables* tt = static_cast<TileTables*>(out);
   std::memset(tt, 0, sizeof(TileTables));
   if (!modal_tables(p, S, (int)tp.tsub, tt)) return kNotFused;  // shared poles: two-launch
+  // The kernels' finite arithmetic uses the flushed taps (common.h,
+  // kTapFlushRel); the caller's own taps go to the kernels' non-finite path.
+  std::vector<float> ft(taps, taps + K);
+  const float thr = tap_flush_threshold(taps, K, L);
+  for (float& t : ft) t = flush_tap(t, thr);
+  tt->flush_thr = thr;
   bool dly = false;
   if (tp.kind == 1) {
-    tap_pairs<Geo3241>(taps, K, tt);
+    tap_pairs<Geo3241>(ft.data(), K, tt);
     dly = delay_branch<Geo3241>(tt);
-  } else gen_sequences(taps, K, L, M, c, tt);
-  if (tp.kind == 3) ct_sequences(taps, K, L, M, c, tt);
+  } else gen_sequences(ft.data(), K, L, M, c, tt);
+  if (tp.kind == 3) ct_sequences(ft.data(), K, L, M, c, tt);
   for (int k = 0; k < kS; ++k) {
     // NORM form (realize() above refused b0 == 0): g = 1, {c1, c2, a1, a2}
     tt->cf[k][0] = p.c[k][1];
@@ -1423,6 +1676,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
                       uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s) {
   TilePlan tp;
   if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
+  DSP_REQUIRE(taps, "null taps");  // the non-finite path reads the caller's taps
   // Tables built for another geometry or cascade: the two-launch chain.  The
   // key also says whether the tables' taps make branch 0 a pure delay.
   const uint64_t key0 = tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
@@ -1466,29 +1720,49 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   a.M = M;
   a.T = (K + L - 1) / L;
   a.win = tp.win;
+  // The repair kernel after the single-pass one (k_chain_*_repair): 64
+  // channels per wave, at most kRepairGroups workgroups.
+  const int64_t groups = tp.kind == 1 ? B : ceil_div(B, (int64_t)kGenWaves);
+  const int64_t rwaves = tp.kind == 1 ? 1 : kGenWaves;
+  const unsigned rgrid =
+      (unsigned)std::min<int64_t>(ceil_div(B, kWave * rwaves), kRepairGroups);
   if (tp.kind == 1) {
-    TraceScope trace("chain_tile", s);
-    auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s, a);
+    {
+      TraceScope trace("chain_tile", s);
+      auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s, a);
+    }
+    TraceScope trace("chain_repair", s);
+    auto rep = dly ? k_chain_tile_repair<Geo3241, true> : k_chain_tile_repair<Geo3241, false>;
+    hipLaunchKernelGGL(rep, dim3(rgrid), dim3(kWave), 0, s, a);
   } else if (tp.kind == 3) {
-    const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
     const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
     auto kern = a.T <= 7 ? k_chain_gct<160, 147, true> : k_chain_gct<160, 147, false>;
+    auto rep = a.T <= 7 ? k_chain_gct_repair<160, 147, true> : k_chain_gct_repair<160, 147, false>;
     if (int rc = allow_lds(kern, shm)) return rc;
-    TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)),
-                       dim3(kWave * kGenWaves), shm, s, a);
+    if (int rc = allow_lds(rep, shm)) return rc;
+    {
+      TraceScope trace("chain_tile", s);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
+                         s, a);
+    }
+    TraceScope trace("chain_repair", s);
+    hipLaunchKernelGGL(rep, dim3(rgrid), dim3(kWave * kGenWaves), shm, s, a);
   } else {
-    DSP_REQUIRE(taps, "null taps");
-    const int64_t groups = ceil_div(B, (int64_t)kGenWaves);
     DSP_REQUIRE(groups * tp.ntiles < ((int64_t)1 << 31), "batch too large for one launch");
     const size_t shm = gen_lds_bytes(tp.win);
     auto kern = M < L ? k_chain_gen<true> : k_chain_gen<false>;
+    auto rep = M < L ? k_chain_gen_repair<true> : k_chain_gen_repair<false>;
     if (int rc = allow_lds(kern, shm)) return rc;
-    TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
-                       s, a);
+    if (int rc = allow_lds(rep, shm)) return rc;
+    {
+      TraceScope trace("chain_tile", s);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
+                         s, a);
+    }
+    TraceScope trace("chain_repair", s);
+    hipLaunchKernelGGL(rep, dim3(rgrid), dim3(kWave * kGenWaves), shm, s, a);
   }
   DSP_LAUNCHED("k_chain_tile");
   return DSP_OK;

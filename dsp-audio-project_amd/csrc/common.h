@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 
@@ -85,6 +86,111 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Taps (include/dspcore.h, dsp_src_polyphase_f32).  The kernels' finite
+// arithmetic uses the caller's float32 taps with every |t| <= kTapFlushRel *
+// max|t| flushed to zero when L > 1: those are the float64 rounding noise of
+// the reference's sinc at its zeros (dsp_core.py:120-129, sinc(k L / L) with
+// |L h| ~ 1e-17 .. 1e-34, and the Blackman window's end taps), below 1e-14 of
+// the signal in y, and flushing them makes the branch that holds the centre
+// tap a pure delay (chain_tile.hip, DLY).  The caller's unflushed taps serve
+// windows that hold an inf or NaN (nonfinite_sum below), so non-finite input
+// propagates as through the reference's float64 convolution.
+constexpr float kTapFlushRel = 1e-12f;
+
+// Largest |t| that is flushed (negative: none, for L == 1).
+inline float tap_flush_threshold(const float* taps, int K, int L) {
+  if (L <= 1) return -1.f;
+  float m = 0.f;
+  for (int k = 0; k < K; ++k) m = fmaxf(m, fabsf(taps[k]));
+  return kTapFlushRel * m;
+}
+
+__host__ __device__ __forceinline__ float flush_tap(float t, float thr) {
+  return fabsf(t) <= thr ? 0.f : t;
+}
+
+// Non-finite inputs.  A window of the reference's convolution that holds an
+// inf or NaN sums to the sum of its non-finite terms alone (finite terms
+// cannot change an inf or a NaN; every reference tap is non-zero): +-inf when
+// the infs that meet a tap agree in sign, NaN otherwise.  window_sums returns,
+// for one output, nf = sum over t of taps[phi + L t] * xn(q - t) with xn = x's
+// non-finite samples (finite ones zeroed) and the caller's unflushed taps --
+// exactly the reference's result when the window holds an inf or NaN, +-0
+// otherwise -- and fin = the kernels' canonical sum of the finite samples with
+// the flushed taps: two FMA chains over x ascending, term t in chain
+// (pb - t) & 1, fin = chain 0 + chain 1 (pb = q for the packed kernels, whose
+// chains follow x's absolute parity; pb = T - 1 for the generic ones, whose
+// chains follow the parity from the window start q - (T - 1)); pb < 0: one
+// chain (the odd-M register-blocked kernel).  xat(t) returns x[q - t].
+template <class XAT>
+__device__ __forceinline__ void window_sums(const float* __restrict__ taps, int K, int L, int phi,
+                                            float thr, int pb, XAT xat, float& nf, float& fin) {
+  float sn = 0.f, c0 = 0.f, c1 = 0.f;
+  // (the tap index in a VGPR even where it is wave-uniform: the rare path runs
+  // inside kernels whose SGPRs are all taken)
+  int t = (K - 1 - phi) / L;
+  asm volatile("" : "+v"(t));
+#pragma unroll 1
+  for (; t >= 0; --t) {
+    const float xv = xat(t), tv = taps[phi + L * t];
+    const bool fx = __builtin_isfinite(xv);
+    sn = fmaf(tv, fx ? 0.f : xv, sn);
+    const float tf = flush_tap(tv, thr), xf = fx ? xv : 0.f;
+    if (pb >= 0 && ((pb - t) & 1)) c1 = fmaf(tf, xf, c1);
+    else c0 = fmaf(tf, xf, c0);
+  }
+  nf = sn;
+  fin = pb >= 0 ? c0 + c1 : c0;
+}
+
+// The rare path's merge for one output: the reference's inf or NaN where the
+// window holds one; else the kernel's sum y, unless that picked up a NaN
+// through a zero tap that meets a neighbouring output's non-finite sample
+// (packed tap pairs and class rows reach one or two samples past an output's
+// window), in which case fin, the same canonical sum without that sample.
+// Returns whether y is non-finite.
+__device__ __forceinline__ bool nf_fix(float& y, float nf, float fin) {
+  if (!__builtin_isfinite(nf)) {
+    y = nf;
+    return true;
+  }
+  if (!__builtin_isfinite(y)) y = fin;
+  return false;
+}
+
+// Class code of a non-finite output (0: finite) and its value back.
+__device__ __forceinline__ int nf_code(float v) {
+  return __builtin_isfinite(v) ? 0 : (v != v ? 3 : (v > 0.f ? 1 : 2));
+}
+__device__ __forceinline__ float nf_value(int code) {
+  return code == 1 ? __builtin_inff() : (code == 2 ? -__builtin_inff() : __builtin_nanf(""));
+}
+
+// fma(x, 0, acc) is NaN exactly when x is an inf or a NaN: accumulating it over
+// the samples a thread loads flags non-finite input at one FMA per two values.
+typedef float nf_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ nf_f32x2 nf_acc(nf_f32x2 acc, float4 v) {
+  const nf_f32x2 z = {0.f, 0.f};
+  acc = __builtin_elementwise_fma(nf_f32x2{v.x, v.y}, z, acc);
+  return __builtin_elementwise_fma(nf_f32x2{v.z, v.w}, z, acc);
+}
+__device__ __forceinline__ bool nf_any(nf_f32x2 acc) { return !__builtin_isfinite(acc.x + acc.y); }
+
+// A state that picked up an inf or NaN becomes all NaN: the reference's
+// cascade (lfilter, DF2T) turns every later output into NaN after a non-finite
+// input (b1 x - a1 y = inf - inf for the peaking sections, whose b1 == a1), and
+// a carried state of +-infs could instead clip to +-1.
+template <int D>
+__device__ __forceinline__ void nf_poison(double (&e)[D]) {
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) s = fma(e[i], 0.0, s);
+  if (!__builtin_isfinite(s)) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) e[i] = __builtin_nan("");
+  }
+}
+
 // Internal launchers shared by the entry points and the fused chain.
 int launch_src(const float* x, float* y, int64_t B, int64_t n_in, int64_t ld_x,
                int64_t n_out, int64_t ld_y, const float* taps, int K, int L,
@@ -124,7 +230,7 @@ int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, in
 // Chain fast path: pass 1 of the fused cascade reads the SRC input xs through
 // the x-domain state table (include/dspcore.h, dsp_chain_xstate_geometry).
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
-                    int64_t* q0, int64_t* rows);
+                    int64_t* q0, int64_t* rows, int64_t* span = nullptr);
 // Single-pass chain (chain_tile.hip): y = SRC(x) and z = clip(cascade(y)) in
 // one launch, y never re-read.  chain_tile_sub returns the sub-chunk length of
 // the instantiated geometry (0: the two-launch chain serves this call).

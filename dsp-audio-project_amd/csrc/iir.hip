@@ -340,6 +340,7 @@ __device__ __forceinline__ void run_pass(const float* __restrict__ x, float* __r
 struct XState {
   const float* xs;  // SRC input rows [B][ld]
   int64_t ld, n, shift, q0, rows;
+  int64_t span;  // rows [0, span) meet a tap of the chunk (Gx is zero beyond)
 };
 
 // Per-wave LDS: the 64 x 33-float tile, reused as the 64 x D-double scan.
@@ -428,7 +429,9 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
     const bool need = c + 1 < C;                          // last chunk: state unused
     s_in[c] = need ? b * XS.ld + start : 0;
     s_lo[c] = need ? (int)max((int64_t)0, -start) : 0;
-    s_len[c] = need ? (int)max((int64_t)0, min(XS.rows, XS.n - start)) : 0;
+    // Only the rows that meet a tap: a non-finite sample past them must not
+    // reach this chunk's state (0 * inf = NaN; it first meets a later chunk).
+    s_len[c] = need ? (int)max((int64_t)0, min(XS.span, XS.n - start)) : 0;
   } else {
     s_in[c] = in2;
     s_lo[c] = 0;
@@ -479,6 +482,8 @@ __global__ __launch_bounds__(kWave * W) void k_iir_wave(
       e[2 * k + 1] = s2[k];
     }
   }
+  // A chunk whose input held an inf or NaN hands NaN on (nf_poison).
+  nf_poison(e);
 
   // ---- carry scan
   block_sync<W>();  // W > 1: the scan slots overlap other waves' tiles
@@ -544,10 +549,17 @@ __global__ __launch_bounds__(kNT) void k_iir_pass(
                                                                s1, s2, e, p, nullptr, clip);
   if (!APPLY && live) {
     double* eo = e_out + g * (2 * S);
+    double ev[2 * SS];
+#pragma unroll
+    for (int k = 0; k < SS; ++k) {
+      ev[2 * k] = s1[k];
+      ev[2 * k + 1] = s2[k];
+    }
+    nf_poison(ev);  // a chunk whose input held an inf or NaN hands NaN on
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      eo[2 * k] = s1[k];
-      eo[2 * k + 1] = s2[k];
+      eo[2 * k] = ev[2 * k];
+      eo[2 * k + 1] = ev[2 * k + 1];
     }
   }
 }
@@ -769,7 +781,7 @@ int run_cascade(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, in
 }  // namespace
 
 int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* shift,
-                    int64_t* q0, int64_t* rows) {
+                    int64_t* q0, int64_t* rows, int64_t* span_out) {
   DSP_REQUIRE(chunk_len > 0 && K >= 1 && L >= 1 && M >= 1 && c >= 0, "bad SRC/chunk geometry");
   DSP_REQUIRE(chunk_len <= ((int64_t)1 << 40) && L <= (1 << 24) && M <= (1 << 24) &&
                   c <= ((int64_t)1 << 40),
@@ -789,6 +801,7 @@ int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* 
   *shift = sh;
   *q0 = lo;
   *rows = ceil_div(span, kTS) * kTS;
+  if (span_out) *span_out = span;
   return DSP_OK;
 }
 
@@ -808,8 +821,9 @@ int launch_biquad_xstate(const float* x, float* y, int64_t B, int64_t n, int64_t
   DSP_REQUIRE(fused_ok(S, ceil_div(n, chunk_len), chunk_len),
               "x-domain states need the fused cascade (n=%lld chunk_len=%lld)", (long long)n,
               (long long)chunk_len);
-  XState XS{xs, ld_xs, n_in, 0, 0, 0};
-  if (int rc = xstate_geometry(chunk_len, K, L, M, c, &XS.shift, &XS.q0, &XS.rows)) return rc;
+  XState XS{xs, ld_xs, n_in, 0, 0, 0, 0};
+  if (int rc = xstate_geometry(chunk_len, K, L, M, c, &XS.shift, &XS.q0, &XS.rows, &XS.span))
+    return rc;
   DSP_REQUIRE(gx_rows == XS.rows, "x-domain state table has %lld rows, geometry needs %lld",
               (long long)gx_rows, (long long)XS.rows);
   DSP_REQUIRE(x && y && sos && xs && gx, "null pointer");

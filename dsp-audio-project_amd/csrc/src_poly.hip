@@ -24,12 +24,14 @@ namespace dsp {
 namespace {
 
 // Fills win[i] = x[qa + i] for i < nload (zeros outside [0, n_in)).
-// qa is a multiple of 4 so aligned rows allow float4 loads.
+// qa is a multiple of 4 so aligned rows allow float4 loads.  Returns whether
+// this thread loaded an inf or NaN (nf_acc).
 template <int NT>
-__device__ __forceinline__ void load_window(float* __restrict__ win,
+__device__ __forceinline__ bool load_window(float* __restrict__ win,
                                             const float* __restrict__ xr,
                                             int64_t qa, int nload, int64_t n_in,
                                             bool vec_ok) {
+  nf_f32x2 nf = {0.f, 0.f};
   const int nv = (nload + 3) >> 2;
   for (int v = threadIdx.x; v < nv; v += NT) {
     const int64_t q = qa + 4 * (int64_t)v;
@@ -43,7 +45,29 @@ __device__ __forceinline__ void load_window(float* __restrict__ win,
       f.w = (q + 3 >= 0 && q + 3 < n_in) ? xr[q + 3] : 0.f;
     }
     *reinterpret_cast<float4*>(win + 4 * v) = f;
+    nf = nf_acc(nf, f);
   }
+  return nf_any(nf);
+}
+
+// Flush threshold of the caller's taps (common.h, kTapFlushRel) for a block of
+// NT threads: the same float32 max and product as tap_flush_threshold, so the
+// device-staged tap banks flush exactly the taps the host tables do.  red:
+// NT / 64 floats of LDS.  Contains a barrier.
+template <int NT>
+__device__ __forceinline__ float block_flush_threshold(const float* __restrict__ taps, int K, int L,
+                                                       float* red) {
+  if (L <= 1) return -1.f;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < K; k += NT) m = fmaxf(m, fabsf(taps[k]));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) r = fmaxf(r, red[w]);
+  return kTapFlushRel * r;
 }
 
 // Writes out[0:count] to yr[0:count] (float4 when the row is aligned).
@@ -98,6 +122,7 @@ __global__ __launch_bounds__(NT) void k_src_reg(
   __shared__ __attribute__((aligned(16))) float s_bank[NROW * TP];
   __shared__ __attribute__((aligned(16))) float s_win[WF];
   __shared__ __attribute__((aligned(16))) float s_out[TILE];
+  __shared__ float s_red[NT / 64];
 
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.y;
@@ -109,7 +134,9 @@ __global__ __launch_bounds__(NT) void k_src_reg(
   const int64_t qhi = ((m0 + TILE - 1) * M + c) / L;
   const int64_t qa = qlo & ~(int64_t)3;
   // Packed pairs reach up to 2 samples past the last window (zero taps there).
-  load_window<NT>(s_win, xr, qa, (int)(qhi - qa + 1 + (PACK ? 2 : 0)), n_in, vec_x != 0);
+  const bool nf = load_window<NT>(s_win, xr, qa, (int)(qhi - qa + 1 + (PACK ? 2 : 0)), n_in,
+                                  vec_x != 0);
+  const float thr = block_flush_threshold<NT>(taps, K, L, s_red);
 
   // Bank row phi holds the branch taps reversed, h[u] = P[phi][T-1-u]; the
   // packed bank has one row per (phi, a): row[k] = h[k - a].
@@ -117,9 +144,9 @@ __global__ __launch_bounds__(NT) void k_src_reg(
     const int row = i / TP, k = i - row * TP;
     const int phi = PACK ? row >> 1 : row, u = PACK ? k - (row & 1) : k;
     const int kk = phi + L * (T - 1 - u);
-    s_bank[i] = (u >= 0 && u < T && kk < K) ? taps[kk] : 0.f;
+    s_bank[i] = (u >= 0 && u < T && kk < K) ? flush_tap(taps[kk], thr) : 0.f;
   }
-  __syncthreads();
+  const bool any_nf = __syncthreads_or(nf);
 
   if (tid < G * L) {
     const int p = tid % L, g = tid / L;
@@ -161,6 +188,20 @@ __global__ __launch_bounds__(NT) void k_src_reg(
     }
   }
   __syncthreads();
+  if (any_nf) {
+    // An inf or NaN in the block's window (rare): every output through
+    // window_sums / nf_fix (common.h) with the caller's taps.
+    for (int i = tid; i < TILE; i += NT) {
+      const int64_t j = (m0 + i) * M + c, q = j / L;
+      const int base = (int)(q - qa);
+      float nfs, fin, v = s_out[i];
+      window_sums(taps, K, L, (int)(j - q * L), thr, PACK ? (int)(q & 1) : -1,
+                  [&](int t) { return s_win[base - t]; }, nfs, fin);
+      nf_fix(v, nfs, fin);
+      s_out[i] = v;
+    }
+    __syncthreads();
+  }
 
   const int64_t count = min((int64_t)TILE, n_out - m0);
   store_tile<NT>(yr + m0, s_out, (int)count, vec_y != 0);
@@ -191,13 +232,15 @@ __global__ __launch_bounds__(kGenNT) void k_src_generic(
   const int64_t qlo = (m0 * M + c) / L - (T - 1);
   const int64_t qhi = ((m1 - 1) * M + c) / L;
   const int64_t qa = qlo & ~(int64_t)3;
-  load_window<kGenNT>(s_win, xr, qa, (int)(qhi - qa + 1), n_in, vec_x != 0);
+  __shared__ float s_red[kGenNT / 64];
+  const bool nf = load_window<kGenNT>(s_win, xr, qa, (int)(qhi - qa + 1), n_in, vec_x != 0);
+  const float thr = block_flush_threshold<kGenNT>(taps, K, L, s_red);
   for (int i = tid; i < L * T; i += kGenNT) {
     const int phi = i / T, u = i - phi * T;
     const int k = phi + L * (T - 1 - u);
-    s_bank[i] = (k < K) ? taps[k] : 0.f;
+    s_bank[i] = (k < K) ? flush_tap(taps[k], thr) : 0.f;
   }
-  __syncthreads();
+  const bool any_nf = __syncthreads_or(nf);
 
   // Output stores are coalesced directly (consecutive threads, consecutive m).
   // (q, phi) of j = m*M + c advance by a fixed (dq, dphi) per iteration, so the
@@ -219,7 +262,14 @@ __global__ __launch_bounds__(kGenNT) void k_src_generic(
       a1 = fmaf(h[u + 1], w[u + 1], a1);
     }
     if (u < T) a0 = fmaf(h[u], w[u], a0);
-    yr[m] = a0 + a1;
+    float v = a0 + a1;
+    if (any_nf) {  // an inf or NaN in the block's window (rare): window_sums / nf_fix
+      const int base = (int)(q - qa);
+      float nfs, fin;
+      window_sums(taps, K, L, phi, thr, T - 1, [&](int t) { return s_win[base - t]; }, nfs, fin);
+      nf_fix(v, nfs, fin);
+    }
+    yr[m] = v;
     q += dq;
     phi += dphi;
     if (phi >= L) {
@@ -274,8 +324,9 @@ int launch_src_rows(const float* x, float* y, int64_t B, int64_t n_in, int64_t l
     const int64_t w = ((int64_t)(t - 1) * M) / L + T + 2 + 8;
     return (int64_t)(bank_floats + ((w + 3) / 4) * 4) * 4;
   };
-  while (tile > 64 && lds_bytes(tile) > 160 * 1024) tile >>= 1;
-  if (lds_bytes(tile) > 160 * 1024)
+  constexpr int64_t kLdsMax = 160 * 1024 - 64;  // (the kernel's static LDS: s_red)
+  while (tile > 64 && lds_bytes(tile) > kLdsMax) tile >>= 1;
+  if (lds_bytes(tile) > kLdsMax)
     return set_error(DSP_ENOTSUP, "tap bank L*ceil(K/L)=%d floats does not fit in LDS", L * T);
   dim3 grid((unsigned)ceil_div(n_out, tile), (unsigned)B);
   const size_t shm = (size_t)lds_bytes(tile);

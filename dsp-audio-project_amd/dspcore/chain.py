@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from .design import (EqPlan, SpectrumPlan, SrcPlan, chunk_len_for, eq_plan, kernel_taps,
+from .design import (EqPlan, SpectrumPlan, SrcPlan, caller_taps, chunk_len_for, eq_plan,
                      max_chunks_for, spectrum_plan, src_plan, xstate_chunk_len)
 
 
@@ -131,7 +131,7 @@ class Chain:
         if self.tile_len > 0:
             nbytes = int(lib.dsp_chain_tile_tables_bytes())
             host = np.zeros(nbytes, dtype=np.uint8)
-            taps32 = np.ascontiguousarray(kernel_taps(self.src))
+            taps32 = caller_taps(self.src)
             key = ctypes.c_uint64(0)
             rc = lib.dsp_chain_tile_tables(
                 host.ctypes.data, nbytes, cfg.n_in, n_out, taps32.ctypes.data, self.src.K,

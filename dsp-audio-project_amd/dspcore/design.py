@@ -84,27 +84,36 @@ def src_plan(n_in: int, fs: int, M: int, L: int, num_taps: int | None = None) ->
     return SrcPlan(L, M, K, h, c, n_in, n_out, int(fs * L / M))
 
 
-# Kernel taps below this fraction of the largest are flushed to exactly zero.
-TAP_FLUSH_REL = 1e-12
+# The library's flush rule (csrc/common.h, kTapFlushRel): taps at or below
+# this fraction of the largest (float32 arithmetic) are zero in its finite sums.
+TAP_FLUSH_REL = np.float32(1e-12)
+
+
+def caller_taps(plan: SrcPlan) -> np.ndarray:
+    """float32 L*h, the taps every SRC entry point of the library takes
+    (include/dspcore.h): the reference's float64 design (dsp_core.py:159-162)
+    rounded once."""
+    return np.ascontiguousarray(np.asarray(plan.taps, dtype=np.float64).astype(np.float32))
 
 
 def kernel_taps(plan: SrcPlan) -> np.ndarray:
-    """float32 L*h as every SRC kernel takes it (ops.taps_tensor, Chain's
-    single-pass tables): the taps at the sinc's zeros -- every L-th tap from the
-    centre when wc = 1/L (upsampling, dsp_core.py:155), whose float64 values are
-    the rounding noise of sin(k pi) (|L h| ~ 1e-17 .. 1e-34 at K = 121) -- are
-    flushed to exactly 0.  Their contribution to y is below 1e-14 of the signal,
-    far inside the SRC tolerance (2e-6), and the polyphase branch that holds
-    the centre tap becomes a pure scaled delay: the single-pass kernel computes
-    its outputs (1/L of them) with one multiply instead of ceil(K/L) FMAs
-    (csrc/chain_tile.hip, DLY), bitwise what the FMA chains give on these taps.
-    The float64 design (generar_respuesta_impulso_sinc) is unchanged; plans
-    with L = 1 (downsampling, and aplicar_ecuacion_diferencias' FIR path) keep
-    every tap as float32(L h)."""
-    t = np.asarray(plan.taps, dtype=np.float64)
-    out = t.astype(np.float32)
-    if plan.L > 1 and t.size:
-        out[np.abs(t) <= TAP_FLUSH_REL * float(np.max(np.abs(t)))] = 0.0
+    """What the library's finite arithmetic makes of caller_taps (a model, for
+    tests: the flush happens inside the library, csrc/common.h): for L > 1 the
+    taps with |t| <= 1e-12 max|t| (float32) are zero -- the taps at the sinc's
+    zeros, every L-th tap from the centre when wc = 1/L (upsampling,
+    dsp_core.py:155), whose float64 values are the rounding noise of sin(k pi)
+    (|L h| ~ 1e-17 .. 1e-34 at K = 121), and the Blackman window's end taps.
+    Their contribution to y is below 1e-14 of the signal, far inside the SRC
+    tolerance (2e-6), and the polyphase branch that holds the centre tap
+    becomes a pure scaled delay: the single-pass kernel computes its outputs
+    (1/L of them) with one multiply instead of ceil(K/L) FMAs
+    (csrc/chain_tile.hip, DLY).  Windows that hold an inf or NaN take the
+    caller's unflushed taps, so non-finite input propagates as through the
+    reference's convolution.  Plans with L = 1 keep every tap."""
+    out = caller_taps(plan).copy()
+    if plan.L > 1 and out.size:
+        thr = TAP_FLUSH_REL * np.max(np.abs(out))
+        out[np.abs(out) <= thr] = 0.0
     return out
 
 

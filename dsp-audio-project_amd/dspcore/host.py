@@ -52,6 +52,11 @@ class HostChain:
         self.n_mag = self.chains[0].mag.shape[1]
         n_in = cfg.n_in
         self.streams = [torch.cuda.Stream(self.device) for _ in range(slots)]
+        # The chains' workspace zero-fill and table uploads were queued on the
+        # current stream; the slot streams (non-blocking) wait for them.
+        setup = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            st.wait_stream(setup)
         self.xpin = [torch.zeros((self.block, n_in), dtype=torch.float32, pin_memory=True)
                      for _ in range(slots)]
         self.xdev = [torch.empty((self.block, n_in), dtype=torch.float32, device=self.device)

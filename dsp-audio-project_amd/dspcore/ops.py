@@ -88,9 +88,10 @@ def ld(x: torch.Tensor) -> int:
 
 
 def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:
-    """The kernels' float32 taps (design.kernel_taps: sinc-zero noise flushed)."""
-    from .design import kernel_taps
-    return torch.from_numpy(kernel_taps(plan)).to(device)
+    """The library's float32 taps (design.caller_taps; it flushes the sinc-zero
+    noise itself, design.kernel_taps)."""
+    from .design import caller_taps
+    return torch.from_numpy(caller_taps(plan)).to(device)
 
 
 def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = None,

@@ -54,9 +54,17 @@ const char* dsp_last_error(void);
  *     j = m*M + c_offset,  phi = j mod L,  q = j div L
  *     y[m] = sum_{t >= 0, phi + L t < K} taps[phi + L t] * x[q - t]
  * with x == 0 outside [0, n_in).  `taps` are the K gain-compensated filter
- * coefficients L*h (dsp_core.py:159-162) already rounded to float32,
+ * coefficients L*h (dsp_core.py:159-162) rounded to float32,
  * c_offset = (min(n_in*L, K) - 1) / 2 ('same' centring),
  * n_out = ceil(max(n_in*L, K) / M).  Accumulation is float32.
+ * Tap flush (ABI 2.1): for L > 1 the sums use every tap with |t| <= 1e-12 *
+ * max|t| (float32) as zero -- the float64 rounding noise of the reference's
+ * sinc at its zeros and the Blackman window's end taps (|L h| ~ 1e-17 ..
+ * 1e-34), which move y by less than 1e-14 per unit input.  Windows that hold
+ * an inf or NaN give the reference's result: +-inf or NaN exactly as
+ * np.convolve with the float64 taps (every one of them non-zero) gives it,
+ * from the caller's unflushed taps; finite outputs beside them keep their
+ * finite sums.
  * ------------------------------------------------------------------------- */
 int dsp_src_polyphase_f32(const float* x, float* y, int64_t B, int64_t n_in,
                           int64_t ld_x, int64_t n_out, int64_t ld_y,
@@ -189,7 +197,12 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * is skipped (a caller that needs z and |Z| alone); anywhere else y == NULL is
  * DSP_EINVAL.  chunk_len, state_table and xstate_table are not used by it; the
  * sos host array only keys the tables (the kernel reads its coefficients from
- * them).
+ * them).  Non-finite input: y, z and mag follow the reference (inf and NaN
+ * as dsp_src_polyphase_f32 gives them; every z after the first non-finite y
+ * of a channel NaN, as lfilter gives it): the single-pass kernel is followed
+ * on `stream` by a repair launch that reruns, with the non-finite semantics,
+ * the tiles of every channel whose carried state became non-finite, and
+ * exits at once when none did.
  *
  * The single-pass kernel hands each tile's end state to the next tile of the
  * channel through the workspace; a wait that polls more than the calling
@@ -214,14 +227,12 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * and the key to every call), 1 when it does not (the two-launch path serves
  * it; nothing to copy; *key = 0), DSP_EINVAL on bad arguments.  With
  * tile_tables == NULL dsp_chain_f32 takes the two-launch path.
- * Delay branch (L3/M2 kernel): when the taps of polyphase branch 0 are all
- * exactly zero but its centre tap (what dspcore.design.kernel_taps makes of
- * the reference's wc = 1/L design: the sinc-zero noise taps, |L h| <= 1e-12
- * max, flushed to 0), the key says so and dsp_chain_f32 computes that
- * branch's outputs (every third) with one multiply each -- bitwise what the
- * FMAs give on those taps.  Raw taps keep a non-zero noise tap there and take
- * the plain kernel.  Pass the same taps to dsp_chain_f32 and to the SRC
- * entry points so y stays bitwise equal across paths.
+ * Delay branch (L3/M2 kernel): when the flushed taps (dsp_src_polyphase_f32)
+ * of polyphase branch 0 are all zero but its centre tap -- as the reference's
+ * wc = 1/L design makes them -- the key says so and dsp_chain_f32 computes
+ * that branch's outputs (every third) with one multiply each, bitwise what the
+ * FMAs give on those taps.  Pass the same taps to dsp_chain_f32 and to the
+ * SRC entry points so y stays bitwise equal across paths.
  *
  * Two-launch path (any other geometry, or dsp_chain_path(1)): SRC, then the
  * cascade.  With `xstate_table` (device, float64 [xstate_rows][2S], may be

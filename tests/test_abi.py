@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20000     # 2.0.0: round 3 changed dsp_chain_f32's arguments
+    assert lib.dsp_version() == 20100     # 2.1.0: the library flushes the caller's taps itself
     assert isinstance(_lib.last_error(), str)
 
 
@@ -206,7 +206,8 @@ def _tables_dtype():
                      ("Q", "<f8", (12, 12)), ("Dp", "<f8", (6, 6, 2, 2)), ("T", "<f8", (12, 12)),
                      ("TP", "<f4", (32, 4, 2)), ("geo", "<i4", (6,)), ("cf", "<f8", (6, 4)),
                      ("gain", "<f8"), ("seq", "<f4", (8, 32, 8)), ("adv", "<u4", (8,)),
-                     ("classes", "<i4"), ("pad", "<i4"), ("seqs", "<f4", (8, 32, 12))],
+                     ("classes", "<i4"), ("pad", "<i4"), ("seqs", "<f4", (8, 32, 12)),
+                     ("flush_thr", "<f4"), ("pad3", "<i4", (3,))],
                     align=True)
 
 
@@ -324,19 +325,23 @@ def test_chain_tile_tables_host_only():
     assert _tables(lib, nbytes, 48008, 72012, taps32.ctypes.data, plan.K, 3, 2, plan.c_offset,
                    _lib.sos_pointer(sos), 6)[2] not in (0, key)
     # tap pairs: branch ph, pair p = (h[2p - a], h[2p + 1 - a]), h[u] = taps[ph + 3 (40 - u)]
+    # of the taps the library flushed itself (design.kernel_taps models it)
+    kt = design.kernel_taps(plan)
+    assert tb["flush_thr"] == np.float32(1e-12) * np.max(np.abs(taps32))
     for ph in range(3):
         a = [((2 * i) // 3) & 1 for i in range(48) if (2 * i) % 3 == ph][0]
-        h = np.array([taps32[ph + 3 * (40 - u)] if 0 <= u < 41 and ph + 3 * (40 - u) < 121
+        h = np.array([kt[ph + 3 * (40 - u)] if 0 <= u < 41 and ph + 3 * (40 - u) < 121
                       else 0.0 for u in range(-1, 43)], dtype=np.float32)
         want = np.array([[h[2 * p - a + 1], h[2 * p + 2 - a]] for p in range(21)])
         np.testing.assert_array_equal(TP[:21, ph], want)
     assert not TP[21:].any() and not TP[:, 3].any()
     c5 = design.src_plan(48000, 44100, 147, 160, 1023)
-    t5 = np.ascontiguousarray(c5.taps, dtype=np.float32)
+    t5c = np.ascontiguousarray(c5.taps, dtype=np.float32)   # what the caller passes
+    t5 = design.kernel_taps(c5)                               # what the tables hold
     # config 5 (generic kernel): 32-sample sub-chunks, no tap pairs (the kernel
     # reads the device taps); 41 taps per branch declines with 1.
     sos5 = np.ascontiguousarray(design.eq_plan(c5.fs_out, gains).sos)
-    rc, tb, key5 = _tables(lib, nbytes, 48000, c5.n_out, t5.ctypes.data, c5.K, 160, 147,
+    rc, tb, key5 = _tables(lib, nbytes, 48000, c5.n_out, t5c.ctypes.data, c5.K, 160, 147,
                            c5.c_offset, _lib.sos_pointer(sos5), 6)
     assert rc == 0 and key5 not in (0, key)
     assert tuple(tb["geo"]) == (32, 0, 160, 147, 1023, 6)

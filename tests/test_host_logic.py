@@ -285,11 +285,12 @@ def test_kernel_taps_flush_only_sinc_zero_noise():
     np.testing.assert_array_equal(design.kernel_taps(fir), fir.taps.astype(np.float32))
 
 
-def test_chain_tile_tables_mark_the_delay_branch():
-    """dsp_chain_tile_tables: with the kernel taps (branch 0 a pure delay) the
-    key differs from the one for the raw float32 taps, both are accepted by
-    the launcher's check (host-only: dsp_chain_tile_len / tables), and a
-    non-zero noise tap in branch 0 takes the plain key."""
+def test_chain_tile_tables_flush_and_mark_the_delay_branch():
+    """dsp_chain_tile_tables flushes the caller's taps itself (csrc/common.h,
+    kTapFlushRel): the reference's float32 taps and design.kernel_taps give
+    byte-identical tables, with branch 0 a pure delay and the DLY key; a
+    branch-0 tap above the flush threshold takes the plain key; a tap at
+    1e-20 is flushed like the sinc-zero noise (host only)."""
     import ctypes
     from dspcore import _lib
     lib = _lib.load()
@@ -297,18 +298,23 @@ def test_chain_tile_tables_mark_the_delay_branch():
     sos = np.ascontiguousarray(design.eq_plan(72000, {"Bass": 6.0}).sos)
     nbytes = lib.dsp_chain_tile_tables_bytes()
 
-    def key_of(t32):
+    def tables(t32):
         buf = np.zeros(nbytes, np.uint8)
         k = ctypes.c_uint64(0)
         rc = lib.dsp_chain_tile_tables(buf.ctypes.data, nbytes, 48000, p.n_out, t32.ctypes.data,
                                        p.K, 3, 2, p.c_offset, _lib.sos_pointer(sos),
                                        sos.shape[0], ctypes.byref(k))
         assert rc == 0
-        return k.value
+        return buf, k.value
 
     kt = np.ascontiguousarray(design.kernel_taps(p))
-    raw = np.ascontiguousarray(p.taps.astype(np.float32))
-    assert np.any(raw[0::3] != 0) and key_of(kt) != key_of(raw)
-    noisy = kt.copy()
+    raw = design.caller_taps(p)
+    assert np.any(raw[0::3] != 0) and np.count_nonzero(kt[0::3]) == 1
+    (bk, kk), (br, kr) = tables(kt), tables(raw)
+    np.testing.assert_array_equal(bk, br)
+    noisy = raw.copy()
     noisy[3] = 1e-20
-    assert key_of(noisy) == key_of(raw)
+    assert tables(noisy)[1] == kr
+    loud = raw.copy()
+    loud[3] = 1e-3
+    assert tables(loud)[1] != kr
