@@ -73,7 +73,8 @@ int dsp_version(void) {
   // 2.1.0: every SRC entry point takes the caller's float32 taps and flushes
   // the sinc-zero noise itself (common.h, kTapFlushRel); inf and NaN input
   // propagate as through the reference's float64 convolution (round 4).
-  return 20100;
+  // 2.2.0: dsp_pcm_batch_to_mono_f32 / dsp_pcm_batch_workspace_bytes (round 4).
+  return 20200;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
@@ -281,6 +282,19 @@ int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double th
   dsp::clear_error();
   return dsp::launch_peak_normalize(x, B, n, ld, threshold, peak_out,
                                     static_cast<hipStream_t>(stream));
+}
+
+size_t dsp_pcm_batch_workspace_bytes(int64_t B, int64_t width) {
+  return dsp::pcm_batch_workspace_bytes(B, width);
+}
+
+int dsp_pcm_batch_to_mono_f32(const void* pcm, size_t pcm_bytes, const dsp_pcm_row* rows,
+                              int64_t B, int64_t width, float* out, int64_t ld_out,
+                              double threshold, uint32_t* peak_out, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_pcm_batch(pcm, pcm_bytes, rows, B, width, out, ld_out, threshold, peak_out,
+                               workspace, workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,

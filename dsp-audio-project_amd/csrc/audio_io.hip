@@ -217,6 +217,114 @@ int absmax(const float* x, int64_t B, int64_t n, int64_t ld, uint32_t* peak, boo
   });
 }
 
+// ---- batched loader (dsp_pcm_batch_to_mono_f32): one decode launch over a
+// table of per-row descriptors, one normalise launch.
+//
+// Launch 1, k_pcm_batch: block (bx, b) decodes + averages row b's frames
+// [bx kIoNT, ...) grid-stride as k_pcm_mono does (the row's format picks the
+// decoder: a block-uniform branch), writes zeros past the row's frames up to
+// the batch width, and stores its max |x| (float bits, k_absmax's order) in
+// its own slot of the block-maxima table -- every slot written, no
+// initialisation, no atomics.  Launch 2, k_scale_batch: each block reduces
+// its row's slots to the peak and divides the row's frames by it where
+// (double)peak > threshold; block 0 stores the peak.
+template <int FMT, int BITS, bool BE, bool S8>
+__device__ __forceinline__ uint32_t pcm_batch_row(const uint8_t* __restrict__ row, int ch,
+                                                  int64_t frames, int64_t width,
+                                                  float* __restrict__ o) {
+  uint32_t m = 0;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < width; i += stride) {
+    const float v = i < frames
+                        ? (float)channel_mean<FMT, BITS, BE, S8>(row + i * (int64_t)ch * (BITS / 8), ch)
+                        : 0.f;
+    o[i] = v;
+    m = max(m, __float_as_uint(v) & 0x7fffffffu);
+  }
+  return m;
+}
+
+// Block-wide unsigned max (kIoNT threads); the result in thread 0.
+__device__ __forceinline__ uint32_t block_umax(uint32_t m, uint32_t* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < kIoNT / 64; ++w) m = max(m, red[w]);
+  return m;
+}
+
+// (format, bits) of a descriptor as one key.
+__host__ __device__ constexpr int pcm_key(int format, int bits) { return format | (bits << 16); }
+
+__global__ __launch_bounds__(kIoNT) void k_pcm_batch(const uint8_t* __restrict__ pcm,
+                                                    const dsp_pcm_row* __restrict__ rows,
+                                                    int64_t b0, int64_t width,
+                                                    float* __restrict__ out, int64_t ld_out,
+                                                    uint32_t* __restrict__ blockmax) {
+  __shared__ uint32_t red[kIoNT / 64];
+  const int64_t b = b0 + blockIdx.y;
+  const dsp_pcm_row r = rows[b];
+  const uint8_t* row = pcm + r.offset;
+  float* o = out + blockIdx.y * ld_out;
+  uint32_t m = 0;
+  switch (pcm_key(r.format, r.bits)) {
+#define DSP_PCMB(F, BI, FLAGS)                                                               \
+  case pcm_key((F) | (FLAGS), BI):                                                           \
+    m = pcm_batch_row<F, BI, ((FLAGS) & DSP_AUDIO_BE) != 0, ((FLAGS) & DSP_AUDIO_S8) != 0>(  \
+        row, r.channels, r.frames, width, o);                                                \
+    break;
+    DSP_PCMB(DSP_WAV_PCM, 8, 0)
+    DSP_PCMB(DSP_WAV_PCM, 8, DSP_AUDIO_S8)
+    DSP_PCMB(DSP_WAV_PCM, 8, DSP_AUDIO_S8 | DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_PCM, 16, 0)
+    DSP_PCMB(DSP_WAV_PCM, 24, 0)
+    DSP_PCMB(DSP_WAV_PCM, 32, 0)
+    DSP_PCMB(DSP_WAV_PCM, 16, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_PCM, 24, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_PCM, 32, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_FLOAT, 32, 0)
+    DSP_PCMB(DSP_WAV_FLOAT, 64, 0)
+    DSP_PCMB(DSP_WAV_FLOAT, 32, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_FLOAT, 64, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_ULAW, 8, 0)
+    DSP_PCMB(DSP_WAV_ALAW, 8, 0)
+    DSP_PCMB(DSP_WAV_ULAW, 8, DSP_AUDIO_BE)
+    DSP_PCMB(DSP_WAV_ALAW, 8, DSP_AUDIO_BE)
+#undef DSP_PCMB
+    default:
+      break;  // the host validated every descriptor
+  }
+  m = block_umax(m, red);
+  if (threadIdx.x == 0) blockmax[b * gridDim.x + blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(kIoNT) void k_scale_batch(float* __restrict__ out, int64_t ld_out,
+                                                      const dsp_pcm_row* __restrict__ rows,
+                                                      int64_t b0, const uint32_t* __restrict__ blockmax,
+                                                      int nbx, double threshold,
+                                                      uint32_t* __restrict__ peak_out) {
+  __shared__ uint32_t red[kIoNT / 64];
+  __shared__ uint32_t pk_bits;
+  const int64_t b = b0 + blockIdx.y;
+  uint32_t m = 0;
+  for (int i = threadIdx.x; i < nbx; i += kIoNT) m = max(m, blockmax[b * nbx + i]);
+  m = block_umax(m, red);
+  if (threadIdx.x == 0) {
+    pk_bits = m;
+    if (blockIdx.x == 0) peak_out[b] = m;
+  }
+  __syncthreads();
+  const float pk = __uint_as_float(pk_bits);
+  if (!((double)pk > threshold)) return;  // NaN peak: unchanged, as in the reference
+  const int64_t frames = rows[b].frames;
+  float* o = out + blockIdx.y * ld_out;
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < frames; i += stride)
+    o[i] = o[i] / pk;
+}
+
 uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 void wr32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
@@ -443,6 +551,95 @@ int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t
   DSP_PCM(DSP_WAV_ALAW, 8, DSP_AUDIO_BE)
 #undef DSP_PCM
   return set_error(DSP_EINVAL, "unsupported sample format 0x%x / %d bits", format, bits);
+}
+
+namespace {
+// Workspace of the batched loader: the device copy of the descriptor table,
+// then the block-maxima table [B][io_blocks(width)].
+struct PcmBatchWs {
+  size_t rows_off, max_off, total;
+};
+PcmBatchWs pcm_batch_ws(int64_t B, int64_t width) {
+  PcmBatchWs w;
+  w.rows_off = 0;
+  const size_t rb = mul_sat((size_t)B, sizeof(dsp_pcm_row));
+  w.max_off = rb == SIZE_MAX ? SIZE_MAX : (rb + 255) & ~(size_t)255;
+  const size_t mb = mul_sat((size_t)B, (size_t)io_blocks(width), sizeof(uint32_t));
+  w.total = (w.max_off == SIZE_MAX || mb == SIZE_MAX) ? SIZE_MAX : add_sat(w.max_off, mb);
+  return w;
+}
+bool pcm_supported(int format, int bits) {
+  switch (pcm_key(format, bits)) {
+    case pcm_key(DSP_WAV_PCM, 8): case pcm_key(DSP_WAV_PCM | DSP_AUDIO_S8, 8):
+    case pcm_key(DSP_WAV_PCM | DSP_AUDIO_S8 | DSP_AUDIO_BE, 8):
+    case pcm_key(DSP_WAV_PCM, 16): case pcm_key(DSP_WAV_PCM, 24): case pcm_key(DSP_WAV_PCM, 32):
+    case pcm_key(DSP_WAV_PCM | DSP_AUDIO_BE, 16): case pcm_key(DSP_WAV_PCM | DSP_AUDIO_BE, 24):
+    case pcm_key(DSP_WAV_PCM | DSP_AUDIO_BE, 32):
+    case pcm_key(DSP_WAV_FLOAT, 32): case pcm_key(DSP_WAV_FLOAT, 64):
+    case pcm_key(DSP_WAV_FLOAT | DSP_AUDIO_BE, 32): case pcm_key(DSP_WAV_FLOAT | DSP_AUDIO_BE, 64):
+    case pcm_key(DSP_WAV_ULAW, 8): case pcm_key(DSP_WAV_ALAW, 8):
+    case pcm_key(DSP_WAV_ULAW | DSP_AUDIO_BE, 8): case pcm_key(DSP_WAV_ALAW | DSP_AUDIO_BE, 8):
+      return true;
+    default:
+      return false;
+  }
+}
+}  // namespace
+
+size_t pcm_batch_workspace_bytes(int64_t B, int64_t width) {
+  if (B <= 0 || width < 0) return 0;
+  return pcm_batch_ws(B, width).total;
+}
+
+int launch_pcm_batch(const void* pcm, size_t pcm_bytes, const dsp_pcm_row* rows, int64_t B,
+                     int64_t width, float* out, int64_t ld_out, double threshold,
+                     uint32_t* peak_out, void* ws, size_t ws_bytes, hipStream_t s) {
+  DSP_REQUIRE(B >= 0 && width >= 0 && ld_out >= width, "bad sizes");
+  if (B == 0) return DSP_OK;
+  DSP_REQUIRE(rows && out && peak_out && ws, "null pointer");
+  for (int64_t b = 0; b < B; ++b) {
+    const dsp_pcm_row& r = rows[b];
+    DSP_REQUIRE(r.channels >= 1 && r.channels <= 128, "row %lld: channels=%d outside [1, 128]",
+                (long long)b, r.channels);
+    DSP_REQUIRE(pcm_supported(r.format, r.bits), "row %lld: unsupported sample format 0x%x / %d bits",
+                (long long)b, r.format, r.bits);
+    DSP_REQUIRE(r.frames >= 0 && r.frames <= width, "row %lld: %lld frames outside [0, width %lld]",
+                (long long)b, (long long)r.frames, (long long)width);
+    const int64_t nbytes = r.frames * r.channels * (r.bits / 8);
+    DSP_REQUIRE(r.offset >= 0 && (uint64_t)r.offset <= pcm_bytes &&
+                    (uint64_t)nbytes <= pcm_bytes - (uint64_t)r.offset,
+                "row %lld: samples [%lld, +%lld) outside the %zu-byte buffer", (long long)b,
+                (long long)r.offset, (long long)nbytes, pcm_bytes);
+    DSP_REQUIRE(nbytes == 0 || pcm, "null pointer");
+  }
+  const PcmBatchWs w = pcm_batch_ws(B, width);
+  DSP_REQUIRE(ws_bytes >= w.total, "loader workspace too small: %zu < %zu bytes", ws_bytes,
+              w.total);
+  DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 255) == 0, "loader workspace not 256-B aligned");
+  char* base = static_cast<char*>(ws);
+  dsp_pcm_row* drows = reinterpret_cast<dsp_pcm_row*>(base + w.rows_off);
+  uint32_t* bmax = reinterpret_cast<uint32_t*>(base + w.max_off);
+  DSP_HIP(hipMemcpyAsync(drows, rows, (size_t)B * sizeof(dsp_pcm_row), hipMemcpyHostToDevice, s));
+  const unsigned nbx = io_blocks(width);
+  if (width == 0) {
+    // nothing to decode: every peak is 0
+    DSP_HIP(hipMemsetAsync(peak_out, 0, (size_t)B * sizeof(uint32_t), s));
+    return DSP_OK;
+  }
+  const uint8_t* p = static_cast<const uint8_t*>(pcm);
+  return for_row_ranges(B, [&](int64_t b0, int64_t nb) {
+    {
+      TraceScope trace("pcm_batch", s);
+      hipLaunchKernelGGL(k_pcm_batch, dim3(nbx, (unsigned)nb), dim3(kIoNT), 0, s, p, drows, b0,
+                         width, out + b0 * ld_out, ld_out, bmax);
+      DSP_LAUNCHED("k_pcm_batch");
+    }
+    TraceScope trace("pcm_batch_scale", s);
+    hipLaunchKernelGGL(k_scale_batch, dim3(nbx, (unsigned)nb), dim3(kIoNT), 0, s,
+                       out + b0 * ld_out, ld_out, drows, b0, bmax, (int)nbx, threshold, peak_out);
+    DSP_LAUNCHED("k_scale_batch");
+    return DSP_OK;
+  });
 }
 
 int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,

@@ -222,6 +222,10 @@ int audio_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);
 int wav_header_pcm16(uint8_t* out, int32_t fs, int32_t channels, int64_t frames);
 int launch_pcm_mono(const void* pcm, int format, int bits, int channels, int64_t B,
                     int64_t frames, int64_t ld_bytes, float* out, int64_t ld_out, hipStream_t s);
+size_t pcm_batch_workspace_bytes(int64_t B, int64_t width);
+int launch_pcm_batch(const void* pcm, size_t pcm_bytes, const dsp_pcm_row* rows, int64_t B,
+                     int64_t width, float* out, int64_t ld_out, double threshold,
+                     uint32_t* peak_out, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
                           uint32_t* peak, hipStream_t s);
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,

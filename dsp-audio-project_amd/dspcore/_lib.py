@@ -81,6 +81,9 @@ _SIGNATURES = {
         _vp, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "dsp_peak_normalize_f32": (ctypes.c_int, [
         _vp, _c_i64, _c_i64, _c_i64, ctypes.c_double, _vp, _vp]),
+    "dsp_pcm_batch_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "dsp_pcm_batch_to_mono_f32": (ctypes.c_int, [
+        _vp, _c_sz, _vp, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_double, _vp, _vp, _c_sz, _vp]),
     "dsp_quantize_pcm16": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _c_i32,
                                           _vp]),
     "dsp_wav_header_pcm16": (ctypes.c_int, [ctypes.c_char_p, _c_i32, _c_i32, _c_i64]),
@@ -102,6 +105,14 @@ class WavInfo(ctypes.Structure):
                 ("sample_rate", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("frames", ctypes.c_int64), ("data_offset", ctypes.c_int64),
                 ("data_bytes", ctypes.c_int64)]
+
+
+class PcmRow(ctypes.Structure):
+    """dsp_pcm_row of include/dspcore.h."""
+    _fields_ = [("offset", ctypes.c_int64), ("frames", ctypes.c_int64),
+                ("format", ctypes.c_int32), ("bits", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
 
 _lock = threading.Lock()
 _lib = None

@@ -303,6 +303,19 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B,
  *                        (double)peak > threshold (the reference uses 1e-6).
  *                        peak_out: caller's device uint32[B], receives the
  *                        peaks as float32 bit patterns.
+ *   dsp_pcm_batch_to_mono_f32  DEVICE: a batch of files in two launches
+ *                        (load_batch): `pcm` (device)
+ *                        holds every row's raw sample bytes, `rows` (HOST,
+ *                        B descriptors: byte offset into pcm, frames, format,
+ *                        bits, channels as dsp_audio_parse gives them; the
+ *                        library validates them against pcm_bytes and copies
+ *                        the table to its workspace) says where; out [B][ld_out]
+ *                        receives row b's dsp_pcm_to_mono_f32 result in
+ *                        [0, frames_b), zeros in [frames_b, width), each row
+ *                        divided by its peak as dsp_peak_normalize_f32 does
+ *                        (threshold, peak_out likewise); workspace (device,
+ *                        256-byte aligned) >= dsp_pcm_batch_workspace_bytes(B,
+ *                        width).  Bitwise the per-file calls.
  * Playback, replacing app.py:349-355 (nan_to_num, divide by max|z| when > 0,
  * * 32767, astype(int16), all in z_final's dtype):
  *   dsp_quantize_pcm16   DEVICE: float32 z [B][ld_z] -> int16 [B][ld_out],
@@ -337,6 +350,19 @@ int dsp_pcm_to_mono_f32(const void* pcm, int32_t format, int32_t bits, int32_t c
                         int64_t ld_out, void* stream);
 int dsp_peak_normalize_f32(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
                            uint32_t* peak_out, void* stream);
+typedef struct dsp_pcm_row {
+  int64_t offset;       /* byte offset of the row's first sample in pcm  */
+  int64_t frames;       /* samples per channel (<= width)                */
+  int32_t format;       /* as dsp_wav_info.format                        */
+  int32_t bits;         /* as dsp_wav_info.bits                          */
+  int32_t channels;     /* 1..128                                        */
+  int32_t reserved;     /* 0                                             */
+} dsp_pcm_row;
+size_t dsp_pcm_batch_workspace_bytes(int64_t B, int64_t width);
+int dsp_pcm_batch_to_mono_f32(const void* pcm, size_t pcm_bytes, const dsp_pcm_row* rows,
+                              int64_t B, int64_t width, float* out, int64_t ld_out,
+                              double threshold, uint32_t* peak_out, void* workspace,
+                              size_t workspace_bytes, void* stream);
 int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
                        int64_t ld_out, uint32_t* peak_out, int32_t precision, void* stream);
 int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,

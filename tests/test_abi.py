@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 28
+    assert len(names) == 30
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20100     # 2.1.0: the library flushes the caller's taps itself
+    assert lib.dsp_version() == 20200     # 2.2.0: the batched loader (2.1.0: the library flushes taps)
     assert isinstance(_lib.last_error(), str)
 
 

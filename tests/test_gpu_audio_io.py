@@ -77,6 +77,78 @@ def test_loader_batch_rows_equal_single_loads(gpu):
         assert not batch[i, lengths[i]:].any()
 
 
+def _mixed_files(rng):
+    """64 files of every layout the loader decodes: WAV PCM 8/16/24/32-bit and
+    IEEE float 32/64 (1-6 channels, lengths 1..5000), every AIFF / AIFF-C /
+    G.711 case of audio_files, silence and a sub-threshold file."""
+    import audio_files
+    files = [f for f, _, _ in audio_files.cases(rng).values()]
+    gens = [
+        lambda n, c: rng.integers(0, 255, (n, c), dtype=np.uint8),
+        lambda n, c: rng.integers(-32768, 32767, (n, c), dtype=np.int16),
+        lambda n, c: rng.integers(-2**31, 2**31 - 1, (n, c), dtype=np.int32),
+        lambda n, c: rng.uniform(-1.3, 1.3, (n, c)).astype(np.float32),
+        lambda n, c: rng.uniform(-2, 2, (n, c)),
+    ]
+    k = 0
+    while len(files) < 60:
+        n, c = int(rng.integers(1, 5000)), int(rng.integers(1, 7))
+        files.append(_wavfile(gens[k % len(gens)](n, c), int(rng.choice([8000, 44100, 48000]))))
+        k += 1
+    files.append(_wav24(rng.integers(-2**23, 2**23 - 1, (1234, 3)), 3, 96000))
+    files.append(_wav24(rng.integers(-2**23, 2**23 - 1, 17), 1, 22050))
+    files.append(_wavfile(np.zeros((321, 2), dtype=np.int16), 44100))
+    files.append(_wavfile((rng.uniform(-1, 1, 999) * 1e-7).astype(np.float32), 44100))
+    return files
+
+
+def test_loader_batch_64_mixed_files_two_launches(gpu):
+    """load_batch of 64 mixed-format files: one host-to-device copy, then
+    dsp_pcm_batch_to_mono_f32's two launches (decode + mean + zero padding,
+    normalise); every row bitwise the per-file load() (the single-file
+    kernels) and the oracle's cargar_senal_audio, zeros past its length."""
+    from dspcore import _lib, audio_io
+    from oracle import dsp_ref_cpu as orc
+    files = _mixed_files(np.random.default_rng(64))
+    assert len(files) == 64
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    try:
+        batch, lengths, rates = audio_io.load_batch(files, gpu)
+        names = [n for n, _ in _lib.trace_read()]
+    finally:
+        _lib.trace_enable(False)
+    assert names == ["pcm_batch", "pcm_batch_scale"]
+    assert batch.shape == (64, max(lengths))
+    got = batch.cpu().numpy()
+    for i, f in enumerate(files):
+        ref, rfs = orc.load_audio(f)
+        assert rates[i] == rfs and lengths[i] == ref.size, i
+        np.testing.assert_array_equal(got[i, :lengths[i]], ref, err_msg=str(i))
+        assert not got[i, lengths[i]:].any(), i
+        one, _ = audio_io.load(f, gpu)
+        assert torch.equal(batch[i, :lengths[i]], one), i
+
+
+def test_loader_batch_rejects_bad_descriptors(gpu):
+    """dsp_pcm_batch_to_mono_f32 validates the host descriptor table: samples
+    outside the buffer, frames past the width, an unknown format."""
+    import ctypes
+    from dspcore import _lib
+    lib = _lib.load()
+    pcm = torch.zeros(64, dtype=torch.uint8, device=gpu)
+    out = torch.empty((1, 16), dtype=torch.float32, device=gpu)
+    peaks = torch.empty(1, dtype=torch.int32, device=gpu)
+    ws = torch.empty(4096, dtype=torch.uint8, device=gpu)
+    for frames, fmt, bits, off in ((16, 1, 16, 40), (17, 1, 8, 0), (4, 5, 16, 0), (4, 1, 12, 0)):
+        d = (_lib.PcmRow * 1)()
+        d[0].offset, d[0].frames, d[0].format, d[0].bits, d[0].channels = off, frames, fmt, bits, 1
+        rc = lib.dsp_pcm_batch_to_mono_f32(pcm.data_ptr(), 64, ctypes.addressof(d), 1, 16,
+                                           out.data_ptr(), 16, 1e-6, peaks.data_ptr(),
+                                           ws.data_ptr(), ws.numel(), None)
+        assert rc == -1, (frames, fmt, bits, off, rc)
+
+
 def test_peak_normalize_nan_and_threshold(gpu):
     from dspcore import audio_io
     x = torch.tensor([[0.5, -2.0, 1.0], [float("nan"), 3.0, 1.0], [1e-7, -5e-7, 0.0]],

@@ -204,7 +204,7 @@ def test_nonfinite_host_chain_matches_reference(gpu, name):
 def test_finite_input_keeps_the_canonical_sums(gpu):
     """The non-finite path is taken only by tiles whose window holds an inf
     or NaN: a row with one NaN gives, in every tile before it, y and z bitwise
-    equal to the same row without it."""
+    equal to the same row without it, and the call after it is unaffected."""
     from dspcore.chain import Chain
     x, _ = _rows("c3")
     clean = x[0:1].copy()
@@ -218,3 +218,9 @@ def test_finite_input_keeps_the_canonical_sums(gpu):
     np.testing.assert_array_equal(y1[0, :first], y0[0, :first])
     np.testing.assert_array_equal(z1[0, :first], z0[0, :first])
     assert np.isnan(z1[0, first + 1:]).all()
+    # the repair leaves no hand-off flag or state behind: a clean call after it
+    # is bitwise the first one
+    y2, z2, _ = (t.cpu().numpy() for t in ch.run(torch.from_numpy(clean).to(gpu)))
+    np.testing.assert_array_equal(y2, y0)
+    np.testing.assert_array_equal(z2, z0)
+    assert ch.handoff_ok()
