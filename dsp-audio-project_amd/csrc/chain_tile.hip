@@ -92,7 +92,11 @@ constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
 constexpr int kNPMax = 32;  // tap pairs per polyphase branch (ceil(K/L) <= 62)
 constexpr int kScanRow = 14;  // doubles per row of the blocked carry scan (12 used)
-constexpr int kScanFloats = 66 * kScanRow * 2;  // its LDS: 64 rows + row 64 + the park row
+// The park row (the tile's entry state) at double 928: dword 1856, a multiple
+// of 64, so lane 0's read of it shares no bank with lane 1's row 1.
+constexpr int kScanPark = 928;
+constexpr int kScanFloats = (kScanPark + 16) * 2;  // its LDS: 64 rows + row 64 + the park row
+                                                   // (+4 doubles idle lanes read)
 
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -338,6 +342,10 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
 // stride TS + 4: conflict-free ds_write_b128), then all 64 lanes store the
 // half's contiguous 32*TS floats.  The buffer resource checks every dword:
 // stores past the row's end are dropped, a float4 across it keeps its head.
+// (The reads take 2-way bank conflicts in some ds_read_b128 lane groups, 48
+// cycles per call at TS = 48; an XOR-swizzled unpadded layout free of them
+// cost more in the VALU that computes its addresses than the LDS cycles it
+// saved: chain 5.73-5.77 vs 5.68-5.70 ms at config 4, same box, round 4.)
 template <int TS>
 __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int lane,
                                            __amdgpu_buffer_rsrc_t rs, int64_t m0) {
@@ -464,7 +472,10 @@ __device__ __forceinline__ void pass1_basis(tt_ptr mt, const f32x2 (&e2)[kD], do
 
 // Pass 2 (file comment, step 5): DF2 entry state s = T m, the cascade rerun
 // over the sub-chunk from it and the clip; y becomes z in place.
-template <int TS>
+// NANCLIP: the clip keeps NaN (v_maximum3/v_minimum3, as np.clip); else one
+// v_med3_f32, which may drop a NaN -- the single-pass kernels' z is finite
+// wherever the repair kernel does not rerun it (tile_cascade).
+template <int TS, bool NANCLIP>
 __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, float (&y)[TS],
                                               const double (&m)[kD]) {
   // s = T m: T is block unit lower triangular (identity diagonal blocks, zero
@@ -500,7 +511,8 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
         const double v2 = fma(c2, s2[k], fma(c1, s1[k], w));
         s2[k] = s1[k];
         s1[k] = w;
-        if (k == kS - 1) y[t] = clip_f32((float)v2, lo, hi);
+        if (k == kS - 1)
+          y[t] = NANCLIP ? clip_f32((float)v2, lo, hi) : __builtin_amdgcn_fmed3f((float)v2, lo, hi);
         else pend[k] = v2;
       }
     }
@@ -611,7 +623,8 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // (144 FMAs + a 24-FMA entry fold, 168 bpermutes).
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   double* rows = reinterpret_cast<double*>(lds);
-  double* park = rows + 65 * kScanRow;
+  double* park = rows + kScanPark;
+  static_assert(kScanPark >= 65 * kScanRow, "park row past the scan rows");
 #pragma unroll
   for (int k = 0; k < kS; ++k)
     *reinterpret_cast<f64x2*>(rows + lane * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
@@ -625,21 +638,27 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     }
   }
   fence();
-  // worker (k, s): lane 8 s + k, k < 6 (lanes 8 s + 6, 8 s + 7 idle; they read
-  // block 0's address, a broadcast).  With this order the b128 row accesses
-  // are free of bank conflicts: a ds_write_b128 group of 8 contiguous lanes is
-  // one segment's 6 blocks, and the ds_read_b128 groups of 16 lanes mix two
-  // segments of each parity on disjoint bank quads (MI355X_MICROARCH.md §LDS).
+  // worker (k, s): lane 8 s + k, k < 6 (lanes 8 s + 6, 8 s + 7 idle: they
+  // read the row's padding slot and the next row's first slot, so that the
+  // 8 lanes of a segment cover 32 consecutive dwords; their results are never
+  // stored).  With this order the b128 row accesses are free of bank
+  // conflicts: a ds_write_b128 group of 8 contiguous lanes is one segment's 6
+  // blocks, and the ds_read_b128 groups of 16 lanes mix two segments of each
+  // parity on disjoint bank quads (MI355X_MICROARCH.md §LDS; round 3's idle
+  // lanes read block 0 of their rows: 32 conflict cycles per wave).
   const int sg = lane >> 3;
   const bool worker = (lane & 7) < 6;
-  const int kb = worker ? (lane & 7) : 0;
+  // (idle lanes load the tables of "blocks" 6 and 7 too: entries of Dp's next
+  // rows, in bounds, never used for a stored value)
+  const int kb = lane & 7;
   const __attribute__((address_space(1))) double* Dg =
       (const __attribute__((address_space(1))) double*)&a.tt->Dp[0][kb][0];
   const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
   const f64x2 d0b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 2);
   f64x2 e[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) e[i] = *reinterpret_cast<const f64x2*>(rows + (8 * sg + i) * kScanRow + 2 * kb);
+  for (int i = 0; i < 8; ++i)
+    e[i] = *reinterpret_cast<const f64x2*>(rows + (8 * sg + i) * kScanRow + 2 * kb);
   const __attribute__((address_space(1))) double* D8g = Dg + 3 * kS * 4;  // Dp[3][kb]
   f64x2 p8a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(D8g);
   f64x2 p8b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(D8g + 2);
@@ -725,7 +744,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     store_tile<TS>(lds, y, lane, ry, m0);
   }
   pin(y);
-  pass2_cascade<TS>(a, mt, y, m);
+  pass2_cascade<TS, REPAIR>(a, mt, y, m);
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
       a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
   int lane_z = lane;

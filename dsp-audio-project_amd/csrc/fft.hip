@@ -686,7 +686,7 @@ __device__ __forceinline__ float2 tw_full(const float2* __restrict__ tw, int64_t
 
 constexpr int kWaveRow = 66;               // transpose row stride (floats): conflict-free both ways
 constexpr int kWaveLds = 32 * kWaveRow;    // floats of LDS per wave
-constexpr int kWavePerGroup = 4;
+constexpr int kWavePerGroup = 16;         // one workgroup per CU (see k_spec_wave12)
 
 // W_128^j = exp(-2 pi i j / 128) for a compile-time j in [0, 128).  oz: an
 // opaque zero OR-ed into the bits, so that the constants are formed where they
@@ -799,14 +799,25 @@ __device__ __forceinline__ void wave_frame_load(const FftArgs& a, int64_t t, int
     raw[n1] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * lane, 512 * n1, 2);
 }
 
-// No prefetch of the next frame: 149 VGPRs and 3 waves per SIMD.  (Holding
-// the next frame in 64 more VGPRs, 2 waves per SIMD, measured 0.199 vs 0.194
-// ms at config 4, profiles/r03_spec_wave_oz_ab.jsonl.)
-__global__ __launch_bounds__(64 * kWavePerGroup)
-__attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
+// The lane's index in its wave, recomputed (mbcnt) and opaque: a fresh copy
+// per use site instead of one register live through the whole loop.
+__device__ __forceinline__ int lane_now() {
+  int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+// No prefetch of the next frame.  (Holding the next frame in 64 more VGPRs,
+// 2 waves per SIMD, measured 0.199 vs 0.194 ms at config 4,
+// profiles/r03_spec_wave_oz_ab.jsonl.)  Round 4: a workgroup is a whole CU's
+// 16 waves sharing one LDS copy of the window (16 KB + 16 transpose buffers =
+// 151 KB), 4 waves per SIMD at <= 128 VGPRs (lane-derived values recomputed
+// per phase, twiddles loaded where used; 4 VGPRs spill, 20 B per lane); round
+// 3's 4-wave groups held the LDS to 3 groups = 3 waves per SIMD: 0.190 vs
+// 0.1955 ms at config 4, 0.0295 vs 0.030 at config 3 (profiles/r04_spec_ab.txt).
+__global__ __launch_bounds__(64 * kWavePerGroup) void k_spec_wave12(FftArgs a) {
   constexpr int N = 4096, NH = 2048;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
-  const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the window, once per workgroup (LDS latency instead of an L2 round trip
   // per transform), then one transpose buffer per wave
@@ -815,49 +826,45 @@ __attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
   __syncthreads();
   const pf2* wl0 = reinterpret_cast<const pf2*>(ldsf);
   float* buf = ldsf + N + wv * kWaveLds;
-  const int hi = lane & 1, k1 = lane >> 1;
-  const int rd = k1 * kWaveRow + hi;        // transpose read base
-  const int src = ((1 - lane) & 63) << 2;   // bpermute address of Z[-K]'s lane
-  const int K0 = k1 + 1024 * hi;
-  const float sg = hi ? -1.f : 1.f;
+  // Lane-derived values are recomputed (lane_now) in each phase of the loop
+  // below instead of held through it: 4 waves per SIMD need <= 128 VGPRs.
   const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
   int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv;
   u32x2_t raw[32];
   for (; t < a.B; t += nw) {
-    wave_frame_load(a, t, lane, raw);
-    // an opaque per-iteration copy of the lane's parity: the combine's 31
-    // per-lane twiddles below are loop-invariant, and hoisting them would
-    // hold 62 VGPRs
-    float hf = (float)hi;
-    asm volatile("" : "+v"(hf));
-    const pf2 hh = pf2{hf, hf};
+    wave_frame_load(a, t, lane_now(), raw);
     // (and of the window and twiddle addresses: hoisted, the window's 32 LDS
     // reads hold 64 VGPRs and the twiddles ~20)
     int z0 = 0;
     asm volatile("" : "+s"(z0));
     const pf2* win = wl0 + z0;
-    const pf2* twp = reinterpret_cast<const pf2*>(a.tw) + z0;
-    const pf2 wl = twp[2 * lane];             // W_2048^lane
-    const pf2 wb = twp[K0];                   // W_4096^K0
-    pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      const int m = (16 * lane * k) & (N - 1);
-      w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
-    }
     pf2 v[32];
+    const int l1 = lane_now();
     // (the window's LDS reads in groups of 8: all 32 in flight would hold 64
     // VGPRs beside the samples)
 #pragma unroll
     for (int n1 = 0; n1 < 32; ++n1) {
       if (n1 % 8 == 0) asm volatile("" ::: "memory");
       v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} *
-              win[64 * n1 + lane];
+              win[64 * n1 + l1];
     }
     // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
     // powers come from the table every 8 steps and by products in between)
     pdft32(v, z0);
     {
+      // the step's twiddles, loaded only now (live through the DFT above
+      // they cost ~10 VGPRs at its peak)
+      int z1 = 0;
+      asm volatile("" : "+s"(z1));
+      const pf2* twp = reinterpret_cast<const pf2*>(a.tw) + z1;
+      const int l2 = lane_now();
+      const pf2 wl = twp[2 * l2];               // W_2048^lane
+      pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const int m = (16 * l2 * k) & (N - 1);
+        w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
+      }
       pf2 p = 0.5f * wl;
       v[0] *= 0.5f;
 #pragma unroll
@@ -871,21 +878,29 @@ __attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
       }
     }
     // T: Y[k1][n2] -> lane 2 k1 + h reads Y[k1][2m + h], one plane at a time
+    const int l3 = lane_now();
+    const int rd = (l3 >> 1) * kWaveRow + (l3 & 1);  // transpose read base
     wave_lds_order();
 #pragma unroll
-    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + lane] = v[k].x;
+    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].x;
     wave_lds_order();
 #pragma unroll
     for (int m = 0; m < 32; ++m) v[m].x = buf[rd + 2 * m];
     wave_lds_order();
 #pragma unroll
-    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + lane] = v[k].y;
+    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].y;
     wave_lds_order();
 #pragma unroll
     for (int m = 0; m < 32; ++m) v[m].y = buf[rd + 2 * m];
     // B: DFT over m, then the radix-2 step across the lane pair: lane h = 1
     // scales its F_1 by W_64^j, the pair swaps, and Z = own * (+-1) + other
     pdft32(v, z0);
+    const int l4 = lane_now();
+    // (the lane's parity as an opaque float: the combine's 31 per-lane
+    // twiddles are loop-invariant, and hoisting them would hold 62 VGPRs)
+    const float hf = (float)(l4 & 1);
+    const pf2 hh = pf2{hf, hf};
+    const float sg = (l4 & 1) ? -1.f : 1.f;
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       pf2 u = v[j];
@@ -896,12 +911,18 @@ __attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
       v[j] = u * sg + pf2{swap_pair(u.x), swap_pair(u.y)};
     }
     // real split and |X[K]|; W_4096^K = W_4096^K0 W_128^j
+    int z2 = 0;
+    asm volatile("" : "+s"(z2));
+    const int l5 = lane_now();
+    const int src = ((1 - l5) & 63) << 2;     // bpermute address of Z[-K]'s lane
+    const int K0 = (l5 >> 1) + 1024 * (l5 & 1);
+    const pf2 wb = (reinterpret_cast<const pf2*>(a.tw) + z2)[K0];  // W_4096^K0
     float* mr = a.out + t * a.ld_out;
     pf2 prev = v[0];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       const pf2 q = pf2{bperm(src, v[31 - j].x), bperm(src, v[31 - j].y)};
-      const pf2 zm = lane < 2 ? prev : q;
+      const pf2 zm = l5 < 2 ? prev : q;
       prev = q;
       const pf2 zk = v[j];
       const pf2 sm = pf2{zk.x + zm.x, zk.y - zm.y};
@@ -909,7 +930,7 @@ __attribute__((amdgpu_waves_per_eu(3))) void k_spec_wave12(FftArgs a) {
       const pf2 x = vcfma(d, pw128(wb, j + 32, z0), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
       mr[K0 + 32 * j] = cabsf_(make_float2(x.x, x.y));
     }
-    if (lane == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
+    if (l5 == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
   }
 }
 
@@ -935,7 +956,7 @@ int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
 // rows (step B) in LDS with the one-launch Stockham passes; the HBM side of
 // both steps moves KC consecutive complex values per index (8 -- 64 B -- for
 // sub-transforms up to 2^11; 4, 2, 1 for 2^12, 2^13, 2^14, whose LDS images
-// are larger: round 3 took the limit from 2^22 to 2^26), staged through LDS so
+// are larger: round 3 took the limit from 2^22 to 2^26, round 4 to 2^28), staged through LDS so
 // every global access is a run of consecutive addresses.  The
 // sub-transforms' twiddles come from the caller's W_N table at stride N/NA
 // (N/NB), the inter-step twiddle W_N^m from the same table (m < N/2, else its
@@ -1051,6 +1072,8 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
     case 24: return launch_fft4<12, 12, MODE>(f, s);
     case 25: return launch_fft4<12, 13, MODE>(f, s);
     case 26: return launch_fft4<13, 13, MODE>(f, s);
+    case 27: return launch_fft4<13, 14, MODE>(f, s);  // (one column per 2^14 workgroup:
+    case 28: return launch_fft4<14, 14, MODE>(f, s);  //  strided, not coalesced, loads)
     default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
   }
 }

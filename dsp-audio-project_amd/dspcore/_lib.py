@@ -29,7 +29,7 @@ DSP_EHIP = -2
 DSP_ENOTSUP = -3
 DSP_MAX_STAGES = 16
 DSP_MAX_LOG2N = 14
-DSP_MAX_LOG2N_FFT = 26
+DSP_MAX_LOG2N_FFT = 28
 DSP_MAX_DFT = 8192
 
 _c_i32, _c_i64, _c_u64, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t

@@ -203,7 +203,7 @@ class LfilterPlan:
     gain: float = 1.0
 
 
-MAX_LFILTER_SECTIONS = 16     # include/dspcore.h DSP_MAX_STAGES: IIR orders up to 32
+MAX_LFILTER_SECTIONS = 16     # include/dspcore.h DSP_MAX_STAGES: sections per cascade launch
 
 
 def lfilter_plan(b, a) -> LfilterPlan:
@@ -214,7 +214,8 @@ def lfilter_plan(b, a) -> LfilterPlan:
     IIR orders are factored into second-order sections with
     scipy.signal.tf2sos (poles and zeros in float64; the cascade is the same
     transfer function as lfilter's direct form II transposed, and better
-    conditioned); IIR orders above 2 * DSP_MAX_STAGES raise RuntimeError.
+    conditioned).  Any order: a cascade of more than DSP_MAX_STAGES sections
+    runs as consecutive launches of up to that many (lfilter_groups).
     """
     b = np.atleast_1d(np.asarray(b, dtype=np.float64))
     a = np.atleast_1d(np.asarray(a, dtype=np.float64))
@@ -235,14 +236,18 @@ def lfilter_plan(b, a) -> LfilterPlan:
     import scipy.signal
     a = np.concatenate([[1.0], a_tail])
     sos6 = scipy.signal.tf2sos(b, a)            # rows b0 b1 b2 a0(=1) a1 a2
-    if sos6.shape[0] > MAX_LFILTER_SECTIONS:
-        raise RuntimeError(
-            f"aplicar_ecuacion_diferencias: order {max(a.size, b.size) - 1} needs "
-            f"{sos6.shape[0]} second-order sections; the GPU cascade takes at most "
-            f"{MAX_LFILTER_SECTIONS}")
     sos = np.ascontiguousarray(np.column_stack([sos6[:, 0:3] / sos6[:, 3:4],
                                                 sos6[:, 4:6] / sos6[:, 3:4]]))
     return LfilterPlan("sos", sos=sos)
+
+
+def lfilter_groups(sos: np.ndarray) -> list[np.ndarray]:
+    """The sections of an 'sos' plan in launch-sized groups (<= DSP_MAX_STAGES
+    rows each), applied in order; between groups the signal is float32 (the
+    cascade kernel's I/O), within a group the state is float64."""
+    sos = np.asarray(sos, dtype=np.float64).reshape(-1, 5)
+    return [sos[g:g + MAX_LFILTER_SECTIONS] for g in range(0, max(1, sos.shape[0]),
+                                                               MAX_LFILTER_SECTIONS)]
 
 
 MAX_FUSED_CHUNKS = 256   # csrc/iir.hip kCBMax: four waves of 64 chunk lanes per channel

@@ -10,7 +10,9 @@ reference names, argument order and meaning (dsp_core.py:10,41,68,104,133,179,
   identity paths return the very same object (SRC with L == M == 1, the EQ
   bypass, an FFT of length <= 1);
 * 2-D numpy [B, n] in -> the same, per row (batched; the reference cannot take
-  2-D signals, so this extends rather than changes its contract);
+  2-D signals, so this extends rather than changes its contract); from
+  SHARD_MIN_ROWS rows on a node with several GPUs the rows are sharded over
+  all of them (bitwise the one-GPU result);
 * a ROCm torch tensor ([n] or [B, n]) in -> a device tensor out, float32 /
   complex64, left on the GPU with no synchronisation.
 
@@ -24,8 +26,8 @@ Deliberate differences, documented in DESIGN.md:
   the tolerances of tests/ (SRC atol 2e-6, EQ atol 1e-5, FFT 1e-5 * max|X|);
 * fft_diezmado_en_tiempo raises ValueError for every length that is not a
   power of two (the reference raises for most and returns a wrong-length
-  array for N = 3), and RuntimeError above 2^26 points (the reference's
-  pure-Python recursion has no limit but takes minutes there);
+  array for N = 3), and RuntimeError above 2^28 points (the reference's
+  pure-Python recursion has no limit but takes hours there);
 * keyword-only extensions: conversion_tasa_muestreo(..., num_taps=None) and
   calcular_espectro_magnitud(..., n_fft=2048); one added function,
   calcular_espectrograma_magnitud (every frame).
@@ -93,6 +95,63 @@ def _from_rows(t, how, np_dtype):
     return host[0] if how == "np1" else host
 
 
+# 2-D numpy batches of at least this many rows use every visible GPU.
+SHARD_MIN_ROWS = 256
+
+
+def _run(x, fn, np_dtype, complex_ok=False):
+    """fn(device rows [b, n], B) -> device rows, applied to x as _to_rows takes
+    it, the result as _from_rows gives it.  A 2-D numpy batch of at least
+    SHARD_MIN_ROWS rows on a node with several GPUs is cut into contiguous row
+    shards, one per visible device (dspcore.shard.shard_ranges), each run from
+    its own host thread; B is the whole batch's row count, so a shard plans as
+    the whole batch does and its rows are bitwise the unsharded ones."""
+    import torch
+    devices = _shard_devices() if not _is_tensor(x) else []
+    if len(devices) > 1 and np.ndim(x) == 2 and np.shape(x)[0] >= SHARD_MIN_ROWS:
+        import threading
+        from dspcore.shard import shard_ranges
+        a = np.asarray(x)
+        B = a.shape[0]
+        host = np.complex64 if complex_ok and np.iscomplexobj(a) else np.float32
+        ranges = shard_ranges(B, len(devices))
+        results: list = [None] * len(ranges)
+        errors: list = []
+
+        def worker(i, lo, hi):
+            try:
+                dev = devices[i]
+                with torch.cuda.device(dev):
+                    t = torch.from_numpy(np.ascontiguousarray(a[lo:hi], dtype=host)).to(dev)
+                    results[i] = fn(t, B).cpu().numpy()
+            except BaseException as e:  # re-raised on the caller's thread
+                errors.append(e)
+
+        threads = [threading.Thread(target=worker, args=(i, lo, hi))
+                   for i, (lo, hi) in enumerate(ranges)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        if errors:
+            raise errors[0]
+        return np.concatenate(results, axis=0).astype(np_dtype)
+    t, how = _to_rows(x, complex_ok)
+    return _from_rows(fn(t, t.shape[0]), how, np_dtype)
+
+
+def _shard_devices():
+    """The devices a large 2-D numpy batch is sharded over: every visible GPU."""
+    import torch
+    return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+
+
+def _cascade(ops, t, sos, clip, B):
+    """The biquad cascade with the chunk length planned for B rows."""
+    chunk = _design.chunk_len_for(int(t.shape[1]), _design.max_chunks_for(B))
+    return ops.biquad_cascade(t, sos, clip=clip, chunk_len=chunk)
+
+
 def _length(x) -> int:
     return int(x.shape[-1]) if (_is_tensor(x) or np.ndim(x) == 2) else len(x)
 
@@ -125,10 +184,10 @@ def cargar_senal_audio(buffer_archivo):
 def fft_diezmado_en_tiempo(x):
     """Radix-2 decimation-in-time FFT (dsp_core.py:41-66), batched HIP kernel.
 
-    Length <= 1 returns x unchanged (:52).  Power-of-two lengths up to 2^26
+    Length <= 1 returns x unchanged (:52).  Power-of-two lengths up to 2^28
     give the natural-order DFT (complex128 for numpy input): one LDS-resident
     launch up to 2^14, a four-step transform (two launches) above.  Other
-    lengths raise ValueError; powers of two above 2^26 raise RuntimeError.
+    lengths raise ValueError; powers of two above 2^28 raise RuntimeError.
     """
     n = _length(x)
     if n <= 1:
@@ -136,8 +195,7 @@ def fft_diezmado_en_tiempo(x):
     if n & (n - 1):
         raise ValueError(f"fft_diezmado_en_tiempo: length {n} is not a power of two")
     ops = _ops()
-    t, how = _to_rows(x, complex_ok=True)
-    return _from_rows(ops.fft(t), how, np.complex128)
+    return _run(x, lambda t, B: ops.fft(t), np.complex128, complex_ok=True)
 
 
 def calcular_espectro_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW):
@@ -148,11 +206,11 @@ def calcular_espectro_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW)
     """
     plan = _design.spectrum_plan(_length(x_n), n_fft)
     ops = _ops()
-    t, how = _to_rows(x_n)
-    mag = ops.spectrum(t, plan.seg_start, plan.seg_len, plan.n_fft)
+    mag = _run(x_n, lambda t, B: ops.spectrum(t, plan.seg_start, plan.seg_len, plan.n_fft),
+               np.float64)
     half = plan.n_fft // 2 + 1
     freqs = np.fft.rfftfreq(plan.n_fft, d=1 / fs)[:half]
-    return freqs, _from_rows(mag, how, np.float64)
+    return freqs, mag
 
 
 def calcular_espectrograma_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW,
@@ -165,11 +223,11 @@ def calcular_espectrograma_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WI
     seconds [frames], magnitudes [frames, N/2+1] -- or [B, frames, N/2+1])."""
     plan = _design.stft_plan(_length(x_n), n_fft, hop)
     ops = _ops()
-    t, how = _to_rows(x_n)
-    mag = ops.stft_magnitude(t, plan.n_fft, plan.hop, plan.frames)
+    mag = _run(x_n, lambda t, B: ops.stft_magnitude(t, plan.n_fft, plan.hop, plan.frames),
+               np.float64)
     freqs = np.fft.rfftfreq(plan.n_fft, d=1 / fs)[:plan.n_fft // 2 + 1]
     times = np.arange(plan.frames) * plan.hop / fs
-    return freqs, times, _from_rows(mag, how, np.float64)
+    return freqs, times, mag
 
 
 # ---------------------------------------------------------------------------
@@ -191,9 +249,7 @@ def conversion_tasa_muestreo(x_n, fs_original, M, L, *, num_taps=None):
         return x_n, fs_original
     plan = _design.src_plan(_length(x_n), fs_original, M, L, num_taps)
     ops = _ops()
-    t, how = _to_rows(x_n)
-    y = ops.src_polyphase(t, plan)
-    return _from_rows(y, how, np.float64), plan.fs_out
+    return _run(x_n, lambda t, B: ops.src_polyphase(t, plan), np.float64), plan.fs_out
 
 
 # ---------------------------------------------------------------------------
@@ -208,24 +264,27 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
     """y = lfilter(b, a, x), zero initial state (dsp_core.py:205-214), any order.
 
     Biquads and second-order sections of higher IIR orders (design.lfilter_plan,
-    float64 on the host) run on the float64 biquad-cascade kernel; a pure FIR
+    float64 on the host) run on the float64 biquad-cascade kernel, 16 sections
+    a launch (float32 between launches, above order 32); a pure FIR
     longer than 3 taps runs as a causal convolution on the SRC kernel (L = M =
     1, float32 taps and sums); b/a of length 1 is a gain.  a[0] == 0 raises
     ValueError as lfilter does.
     """
     plan = _design.lfilter_plan(b, a)
     ops = _ops()
-    t, how = _to_rows(x_n)
-    if plan.kind == "fir":
-        n = int(t.shape[1])
-        src = _design.SrcPlan(1, 1, int(plan.taps.size), plan.taps, 0, n, n, 0)
-        y = ops.src_polyphase(t, src)
-    elif plan.kind == "gain":
-        # one exact-product pass: the cascade kernel with the gain as b0
-        y = ops.biquad_cascade(t, np.array([[plan.gain, 0.0, 0.0, 0.0, 0.0]]), clip=False)
-    else:
-        y = ops.biquad_cascade(t, plan.sos, clip=False)
-    return _from_rows(y, how, np.float64)
+
+    def run(t, B):
+        if plan.kind == "fir":
+            n = int(t.shape[1])
+            src = _design.SrcPlan(1, 1, int(plan.taps.size), plan.taps, 0, n, n, 0)
+            return ops.src_polyphase(t, src)
+        if plan.kind == "gain":
+            # one exact-product pass: the cascade kernel with the gain as b0
+            return _cascade(ops, t, np.array([[plan.gain, 0.0, 0.0, 0.0, 0.0]]), False, B)
+        for group in _design.lfilter_groups(plan.sos):   # any order: <= 16 sections a launch
+            t = _cascade(ops, t, group, False, B)
+        return t
+    return _run(x_n, run, np.float64)
 
 
 def sistema_ecualizador(x_n, fs, ganancias_bandas):
@@ -234,11 +293,9 @@ def sistema_ecualizador(x_n, fs, ganancias_bandas):
     if plan.bypass:
         return x_n
     ops = _ops()
-    t, how = _to_rows(x_n)
-    z = ops.biquad_cascade(t, plan.sos, clip=True)
     if plan.sos.shape[0] > 0:
         out_dtype = np.float64
     else:  # no stage applied: np.clip of x_n.copy() keeps a floating dtype
         dt = np.asarray(x_n).dtype if not _is_tensor(x_n) else np.float32
         out_dtype = dt if np.issubdtype(dt, np.floating) else np.float64
-    return _from_rows(z, how, out_dtype)
+    return _run(x_n, lambda t, B: _cascade(ops, t, plan.sos, True, B), out_dtype)

@@ -37,7 +37,7 @@ extern "C" {
 
 #define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
-#define DSP_MAX_LOG2N_FFT 26 /* largest FFT / spectrum (four-step above 2^14)  */
+#define DSP_MAX_LOG2N_FFT 28 /* largest FFT / spectrum (four-step above 2^14)  */
 #define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
 
 /* ABI version (major*10000 + minor*100 + patch). */

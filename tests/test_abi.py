@@ -26,13 +26,15 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     lib = _lib.load()
     rc = lib.dsp_src_polyphase_f32(None, None, 1, 10, 10, 10, 10, None, 121, 0, 2, 0, None)
     assert rc == _lib.DSP_EINVAL and "L=0" in _lib.last_error()
-    rc = lib.dsp_fft_c2c_f32(None, None, 1, 27, 1, 1 << 27, 1 << 27, None, None, 0, None)
+    rc = lib.dsp_fft_c2c_f32(None, None, 1, 29, 1, 1 << 29, 1 << 29, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL
     # four-step sizes need a workspace of B * N complex
     assert lib.dsp_fft_workspace_bytes(3, 14) == 0
     assert lib.dsp_fft_workspace_bytes(3, 15) == 3 * (1 << 15) * 8
     assert lib.dsp_fft_workspace_bytes(3, 26) == 3 * (1 << 26) * 8
-    assert lib.dsp_fft_workspace_bytes(3, 27) == 0
+    assert lib.dsp_fft_workspace_bytes(1, 28) == (1 << 28) * 8
+    assert lib.dsp_fft_workspace_bytes(1, 29) == 0
+    assert lib.dsp_fft_workspace_bytes(3, 27) == 3 * (1 << 27) * 8
     rc = lib.dsp_fft_c2c_f32(1024, 1024, 1, 15, 1, 1 << 15, 1 << 15, 1024, None, 0, None)
     assert rc == _lib.DSP_EINVAL and "workspace" in _lib.last_error()
     sos = (ctypes.c_double * 5)(1, 0, 0, 0, 0)

@@ -176,14 +176,15 @@ def test_single_biquad_matches_lfilter(gpu):
 def test_difference_equation_any_order_matches_lfilter(gpu):
     """aplicar_ecuacion_diferencias for any (b, a), as lfilter takes them
     (reference dsp_core.py:214): orders 1-8 (Butterworth, Chebyshev, elliptic,
-    random stable), b longer than a, a[0] != 1, FIRs, a pure gain -- within
+    random stable), orders 36 and 48 (18 and 24 sections: two cascade
+    launches), b longer than a, a[0] != 1, FIRs, a pure gain -- within
     1e-5 of scipy.signal.lfilter (relative to max|y| when that exceeds 1), 1-D
     numpy in -> float64 out, 2-D batches per row."""
     import scipy.signal
-    from test_host_logic import _lfilter_cases
+    from test_host_logic import _high_order_cases, _lfilter_cases
     dc = _dc()
     x = np.random.default_rng(5).uniform(-1, 1, (2, 20000))
-    for name, b, a in _lfilter_cases():
+    for name, b, a in _lfilter_cases() + _high_order_cases():
         ref = scipy.signal.lfilter(b, a, x[0])
         y = dc.aplicar_ecuacion_diferencias(x[0], b, a)
         assert y.dtype == np.float64 and y.shape == ref.shape
@@ -670,6 +671,43 @@ def test_chain_config5_full_batch_and_shards(gpu):
         del sh, ys, zs, ms
 
 
+def test_drop_in_shards_large_batches(gpu, monkeypatch):
+    """The drop-in's 2-D numpy calls from SHARD_MIN_ROWS rows run on every
+    visible GPU (here four shards on the one card): SRC, EQ (chunk length
+    planned for the whole batch), lfilter, FFT and spectrum rows bitwise the
+    one-device results; below the threshold nothing is sharded."""
+    dc = _dc()
+    rng = np.random.default_rng(31)
+    B = dc.SHARD_MIN_ROWS + 3
+    x = rng.uniform(-0.9, 0.9, (B, 4800)).astype(np.float32)
+    gains = {"Sub-Bass": 6, "Bass": -3, "Low Mids": 2, "High Mids": 0, "Presence": 4,
+             "Brilliance": -6}
+
+    def calls():
+        y, fs = dc.conversion_tasa_muestreo(x, 48000, 2, 3)
+        z = dc.sistema_ecualizador(y, fs, gains)
+        w = dc.aplicar_ecuacion_diferencias(x, [0.2, 0.3, 0.1], [1.0, -0.5, 0.25])
+        X = dc.fft_diezmado_en_tiempo(x[:, :4096])
+        _, m = dc.calcular_espectro_magnitud(z, fs)
+        return y, z, w, X, m
+
+    monkeypatch.setattr(dc, "_shard_devices", lambda: [gpu])
+    one = calls()
+    monkeypatch.setattr(dc, "_shard_devices", lambda: [gpu] * 4)
+    four = calls()
+    for a, b in zip(one, four):
+        assert a.dtype == b.dtype and a.shape == b.shape
+        np.testing.assert_array_equal(a, b)
+    # a sharded call never takes the one-device route (_to_rows); a smaller one does
+    got = []
+    orig = dc._to_rows
+    monkeypatch.setattr(dc, "_to_rows", lambda *a, **k: got.append(1) or orig(*a, **k))
+    dc.conversion_tasa_muestreo(x, 48000, 2, 3)
+    assert not got
+    dc.conversion_tasa_muestreo(x[:dc.SHARD_MIN_ROWS - 1], 48000, 2, 3)
+    assert got
+
+
 def test_shards_plan_with_the_job_batch(gpu):
     """Two-launch geometry (config 5's L/M = 160/147), 4096 rows: planned with
     the job's batch (Chain(plan_batch=4096)) every shard of 1, 2 and 4 runs the
@@ -704,8 +742,9 @@ def test_shards_plan_with_the_job_batch(gpu):
 def test_fft_four_step_matches_reference(gpu):
     """N = 2^13 .. 2^16 through the drop-in against the reference's own outputs
     (tests/golden/fft_large.npz; 2^15 and 2^16 take the four-step path), and
-    2^17 .. 2^22 batched and 2^23 / 2^24 / 2^26 against np.fft.fft:
-    max|dX| <= 1e-5 * max|X|; 2^27 raises RuntimeError."""
+    2^17 .. 2^22 batched and 2^23 / 2^24 / 2^26 against np.fft.fft, 2^27 and
+    2^28 against the exact DFT of a sum of tones: max|dX| <= 1e-5 * max|X|;
+    2^29 raises RuntimeError."""
     dc = _dc()
     g = golden("fft_large")
     for k in (13, 14, 15, 16):
@@ -740,8 +779,30 @@ def test_fft_four_step_matches_reference(gpu):
         err = np.max(np.abs(X - ref))
         assert err <= FFT_RTOL * np.max(np.abs(ref)), (lg, err)
         del X, ref
+    # 2^27 and 2^28 (round 4: 2^13 x 2^14 and 2^14 x 2^14): a sum of tones,
+    # whose DFT is known exactly (N a_j at bin f_j, zero elsewhere), built and
+    # checked on the device
+    for lg in (27, 28):
+        n = 1 << lg
+        f = torch.tensor([1, 12345, n // 3, n - 7], dtype=torch.int64, device=gpu)
+        amp = torch.tensor([0.5, -0.25 + 0.5j, 0.75j, 0.3], dtype=torch.complex128, device=gpu)
+        idx = torch.arange(n, dtype=torch.int64, device=gpu)
+        x = torch.zeros(n, dtype=torch.complex64, device=gpu)
+        for fj, aj in zip(f, amp):
+            ph = ((fj * idx) % n).double() * (2 * np.pi / n)
+            x += (aj * torch.polar(torch.ones_like(ph), ph)).to(torch.complex64)
+            del ph
+        del idx
+        X = _ops().fft(x[None, :])[0]
+        del x
+        want = torch.zeros(n, dtype=torch.complex64, device=gpu)
+        want[f] = (n * amp).to(torch.complex64)
+        err = float(torch.max(torch.abs(X - want)))
+        assert err <= FFT_RTOL * n * 0.75, (lg, err)
+        del X, want
+        torch.cuda.empty_cache()
     with pytest.raises(RuntimeError):
-        _ops().fft(torch.zeros((1, 1 << 27), device=gpu))
+        _ops().fft(torch.zeros((1, 1 << 29), dtype=torch.complex64, device=gpu))
 
 
 def test_spectrum_four_step_matches_reference(gpu):

@@ -252,8 +252,35 @@ def test_lfilter_plan_any_order_matches_lfilter():
         assert np.max(np.abs(got - ref)) <= 1e-9 * max(1.0, np.max(np.abs(ref))), name
     with pytest.raises(ValueError, match="a\\[0\\] == 0"):
         design.lfilter_plan([1.0], [0.0, 1.0])
-    with pytest.raises(RuntimeError, match="sections"):
-        design.lfilter_plan([1.0], np.poly(0.5 * np.ones(34)))
+    # any order (round 4): more than DSP_MAX_STAGES sections run in groups
+    for name, b, a in _high_order_cases():
+        plan = design.lfilter_plan(b, a)
+        groups = design.lfilter_groups(plan.sos)
+        assert plan.kind == "sos" and plan.sos.shape[0] > design.MAX_LFILTER_SECTIONS
+        assert all(g.shape[0] <= design.MAX_LFILTER_SECTIONS for g in groups)
+        assert np.array_equal(np.concatenate(groups), plan.sos)
+        got = x
+        for g in groups:
+            got = ss.sosfilt(np.column_stack([g[:, :3], np.ones(g.shape[0]), g[:, 3:]]), got)
+        ref = ss.lfilter(b, a, x)
+        assert np.max(np.abs(got - ref)) <= 1e-9 * max(1.0, np.max(np.abs(ref))), name
+
+
+def _high_order_cases():
+    """IIR orders 36 and 48 from random stable sections (pole radius <= 0.85:
+    lfilter's direct form stays accurate there, unlike a Butterworth of that
+    order)."""
+    import scipy.signal as ss
+    rng = np.random.default_rng(21)
+    out = []
+    for order in (36, 48):
+        secs = []
+        for _ in range(order // 2):
+            r, th = rng.uniform(0.3, 0.85), rng.uniform(0.1, 3.0)
+            secs.append([1.0, rng.uniform(-1, 1), rng.uniform(-0.5, 0.5), 1.0,
+                         -2 * r * np.cos(th), r * r])
+        out.append((f"random stable order {order}", *ss.sos2tf(np.array(secs))))
+    return out
 
 
 def test_kernel_taps_flush_only_sinc_zero_noise():
