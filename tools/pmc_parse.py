@@ -17,6 +17,10 @@ from collections import defaultdict
 
 def short(name):
     """Bench-trace name of a libdspcore kernel from its demangled symbol."""
+    if "_repair" in name:
+        return "chain_repair"
+    if "k_pcm_batch" in name or "k_scale_batch" in name:
+        return "pcm_batch"
     if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gct" in name:
         return "chain_tile"
     if "k_tile_prep" in name:
