@@ -337,18 +337,32 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
   }
 }
 
+// Row (g div TS) of output float g = 4 (lane + 64 k) in store_tile's staging.
+template <int TS>
+__device__ __forceinline__ int stage_row(int lane, int k) {
+  if constexpr (TS == 32) {
+    return (lane >> 3) + 8 * k;                       // (lane + 64 k) div 8
+  } else {
+    static_assert(TS == 48, "staging rows of 8 or 12 float4s");
+    // (lane + 64 k) div 12 = 5 k + (lane + 4 k) div 12, and v div 12 = (43 v) >> 9
+    // for v < 131 (lane + 4 k < 88)
+    return 5 * k + (((lane + 4 * k) * 43) >> 9);
+  }
+}
+
 // Stores the tile's 64 x TS outputs (lane l holds outputs l*TS + i) as
-// coalesced float4s: each half of the lanes writes its rows into LDS (row
-// stride TS + 4: conflict-free ds_write_b128), then all 64 lanes store the
-// half's contiguous 32*TS floats.  The buffer resource checks every dword:
-// stores past the row's end are dropped, a float4 across it keeps its head.
+// coalesced float4s through `rs`, a buffer resource whose base is the tile's
+// first output: each half of the lanes writes its rows into LDS (row stride
+// TS + 4: conflict-free ds_write_b128), then all 64 lanes store the half's
+// contiguous 32*TS floats.  The resource checks every dword: stores past the
+// row's end are dropped, a float4 across it keeps its head.
 // (The reads take 2-way bank conflicts in some ds_read_b128 lane groups, 48
 // cycles per call at TS = 48; an XOR-swizzled unpadded layout free of them
 // cost more in the VALU that computes its addresses than the LDS cycles it
 // saved: chain 5.73-5.77 vs 5.68-5.70 ms at config 4, same box, round 4.)
 template <int TS>
 __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int lane,
-                                           __amdgpu_buffer_rsrc_t rs, int64_t m0) {
+                                           __amdgpu_buffer_rsrc_t rs) {
   constexpr int RS = TS + 4;
   constexpr int NF4 = (kWave / 2) * TS / 4;
   static_assert(NF4 % kWave == 0, "whole float4 rounds per half");
@@ -366,16 +380,16 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
     fence();
 #pragma unroll
     for (int k = 0; k < NF4 / kWave; ++k) {
+      // output float g = 4 (lane + 64 k) sits in row r = g div TS at r RS + g
+      // mod TS = g + 4 r; r from a multiply-shift (no 32-bit division)
       const int g = 4 * (lane + kWave * k);
-      const int r = g / TS, c = g - r * TS;
-      const float4 f = *reinterpret_cast<const float4*>(lds + r * RS + c);
+      const float4 f = *reinterpret_cast<const float4*>(lds + g + 4 * stage_row<TS>(lane, k));
       u32x4 d;
       d.x = __float_as_uint(f.x);
       d.y = __float_as_uint(f.y);
       d.z = __float_as_uint(f.z);
       d.w = __float_as_uint(f.w);
-      const int64_t off = (m0 + (int64_t)h * (kWave / 2) * TS + g) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, kStream);
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (h * (kWave / 2) * TS + g) * 4, 0, kStream);
     }
   }
   fence();
@@ -425,7 +439,7 @@ __device__ __forceinline__ void pass1_state(tt_ptr mt, const float (&y)[TS], dou
     // (samples 2j, 2j+1 against the row pair Gc[j][d]) ...
     f32x2 e2[kD];
 #pragma unroll
-    for (int d = 0; d < kD; ++d) e2[d] = f32x2{0.f, 0.f};
+    for (int d = 0; d < kD; ++d) e2[d] = f32x2{-0.f, -0.f};  // (-0: the first FMA is a multiply)
 #pragma unroll
     for (int j = 0; j < TS / 2; ++j) {
       // Each row pair's 24 floats are scalar-loaded right before its FMAs (an
@@ -738,18 +752,20 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 
   // ---- 5. y out (unless the caller passed y = NULL), DF2 entry state
   // s = T m, pass 2, z out
+  // (the buffer resources start at the tile's first output, so that the store
+  // offsets are lane- and k-terms only; their size keeps the row-end checks)
   if (YST && a.y) {
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        a.y + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
-    store_tile<TS>(lds, y, lane, ry, m0);
+        a.y + b * a.ld_y + m0, 0, (int)((a.n_out - m0) * 4), 0x00020000);
+    store_tile<TS>(lds, y, lane, ry);
   }
   pin(y);
   pass2_cascade<TS, REPAIR>(a, mt, y, m);
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
-      a.z + b * a.ld_y, 0, (int)(a.n_out * 4), 0x00020000);
+      a.z + b * a.ld_y + m0, 0, (int)((a.n_out - m0) * 4), 0x00020000);
   int lane_z = lane;
   asm volatile("" : "+v"(lane_z));  // recompute the store offsets (no spill across pass 2)
-  store_tile<TS>(lds, y, lane_z, rz, m0);
+  store_tile<TS>(lds, y, lane_z, rz);
 }
 
 // Repair kernels (k_chain_*_repair), launched after every single-pass kernel
@@ -818,15 +834,20 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
         const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
     const int64_t xs0 = m0 * GEO::M / GEO::L + a.cq - (GEO::TT - 1);  // multiple of 4
     constexpr int NF = GEO::NWIN / 4;
+    // The lane's float4s f = lane + 64 k: buffer byte (xs0 + 4 f) * 4 = off0 +
+    // 1024 k and LDS float xpad(4 f) = l0 + 288 k (lane < 64), one address
+    // register each with k in the instructions' offsets.
+    const int off0 = (int)(xs0 * 4) + 16 * lane;
+    float* const l0 = lds + 4 * lane + 4 * (lane >> 3);
 #pragma unroll
     for (int k = 0; k < (NF + kWave - 1) / kWave; ++k) {
-      const int f = lane + kWave * k;
-      if ((k + 1) * kWave <= NF || f < NF) {
+      if ((k + 1) * kWave <= NF || lane + kWave * k < NF) {
         // "Negative" offsets (tile 0) are >= 2^31 as unsigned: out of range, zeros.
-        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((xs0 + 4 * f) * 4), 0, kStream);
-        *reinterpret_cast<f32x4*>(lds + xpad(4 * f)) = v;
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off0 + 1024 * k, 0, kStream);
+        *reinterpret_cast<f32x4*>(l0 + 288 * k) = v;
       }
     }
+    static_assert(xpad(4 * (kWave + 7)) - xpad(4 * 7) == 288, "xpad: 288 floats per 64 float4s");
   }
   fence();  // one wave: its LDS operations execute in order
 
