@@ -395,14 +395,12 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
   fence();
 }
 
-// Entry state of the tile: lane 0 waits for the previous tile of the channel
-// (hand-off, file comment) and loads its end state; zero for tile 0 and for
-// the other lanes.
+// Entry state of a tile > 0: lane 0 waits for the previous tile of the
+// channel (hand-off, file comment) and loads its end state into m_in (the
+// other lanes leave m_in unset).
 __device__ __forceinline__ void tile_entry_state(const TileArgs& a, int64_t b, int64_t tile,
                                                  int lane, double (&m_in)[kD]) {
-#pragma unroll
-  for (int d = 0; d < kD; ++d) m_in[d] = 0.0;
-  if (tile > 0 && lane == 0) {
+  if (lane == 0) {
     const int64_t prev = b * a.ntiles + tile - 1;
     uint32_t spins = 0;
     bool ok = true;
@@ -642,8 +640,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #pragma unroll
   for (int k = 0; k < kS; ++k)
     *reinterpret_cast<f64x2*>(rows + lane * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
-  // The tile's entry state (hand-off wait; lane 0) goes to the park row.
-  {
+  // The tile's entry state (hand-off wait; lane 0) goes to the park row
+  // (tile 0: zeros, one zero register pair for all six stores).
+  if (tile == 0) {
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < kS; ++k) *reinterpret_cast<f64x2*>(park + 2 * k) = f64x2{0.0, 0.0};
+    }
+  } else {
     double m_in[kD];
     tile_entry_state(a, b, tile, lane, m_in);
     if (lane == 0) {
@@ -716,14 +720,18 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     u0 = ss >= 0 ? x0 : mi.x;
     u1 = ss >= 0 ? x1 : mi.y;
   }
+  // (every lane stores: the idle lanes 6 and 7 of a segment both to the
+  // row's padding slot 6 -- no exec masking per row, one address register)
+  f64x2* const wr = reinterpret_cast<f64x2*>(rows + (8 * sg + 1) * kScanRow) + (kb < 6 ? kb : 6);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const double n0 = fma(d0a.x, u0, fma(d0a.y, u1, e[i].x));
     const double n1 = fma(d0b.x, u0, fma(d0b.y, u1, e[i].y));
     u0 = n0;
     u1 = n1;
-    if (worker) *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * kb) = f64x2{u0, u1};
+    wr[i * (kScanRow / 2)] = f64x2{u0, u1};
   }
+  static_assert(kScanRow == 14, "six blocks and one padding slot per scan row");
   // ---- 4. publish the tile's end state (segment 7's workers hold v_63); the
   // channel's last tile too, for the repair kernel (no flag: nobody waits)
   {
@@ -1005,13 +1013,14 @@ __device__ __forceinline__ void chain_gen_body(const TileArgs& a, const float* s
   // (output i+1's LDS reads are issued before output i's FMAs).  UP (M < L):
   // q advances by 0 or 1 per output, so the 8-sample window slides in
   // registers and one new sample is read per output; otherwise all 8 are read.
+  // (j = m M + c in 32 bits: tile_geometry keeps n_out M + c below 2^31)
   float y[kGenTS];
   const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
   {
-    const int64_t q0 = j0 / L;
-    int qr = (int)(q0 - (T - 1) - qa);  // window offset of the output's first tap
+    const int jl = (int)(m0 * M + a.c) + kGenTS * M * lane;
+    int qr = jl / L - (T - 1) - (int)qa;  // window offset of the output's first tap
     const int dq = M / L;
-    const int cls = (int)((tile * kWave + lane) % C);  // sub-chunk j = m0/32 + lane
+    const int cls = ((int)tile * kWave + lane) % C;  // sub-chunk j = m0/32 + lane
     const float* row = seq + cls * kGenClassStride;   // output i's taps at row + 8 i
     const uint32_t am = adv[cls];
     float w[kGenTT];
@@ -1117,6 +1126,8 @@ __global__ __launch_bounds__(kWave * kGenWaves) void k_chain_gen_repair(TileArgs
 // T7 (T <= 7 taps per branch, config 5's K = 1023): an output whose g_i is
 // even has shift d_i in {0, 1}, so its taps fill slots 0..7 and slots 8, 9 are
 // zero: the last tap-pair read and FMA are skipped (bitwise the same y).
+constexpr int ct_gcd(int a, int b) { return b ? ct_gcd(b, a % b) : a; }
+
 // Class rows of k_chain_gct into LDS (the C classes in use only).  Ends with
 // a workgroup barrier.
 __device__ __forceinline__ void ct_load_classes(const TileArgs& a, float* seq) {
@@ -1139,7 +1150,9 @@ __device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* s
   constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
   const int T = a.T;
   const tt_ptr mt = (tt_ptr)a.tt;
-  const int C = mt->classes;
+  // the phase classes of the 32-output sub-chunk starts, known at compile
+  // time for the ratio (gen_classes; the host checked the tables hold as many)
+  constexpr int C = L / ct_gcd((kGenTS * M) % L, L);
   const int64_t m0 = tile * kGenTile;
 
   // ---- x window of the tile
@@ -1149,11 +1162,13 @@ __device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* s
   fence();
 
   // ---- 1. SRC of the lane's 32 outputs from its register window
+  // (j = m M + c in 32 bits: tile_geometry keeps n_out M + c below 2^31)
   float y[kGenTS];
   const int64_t j0 = (m0 + (int64_t)kGenTS * lane) * M + a.c;
   {
-    const float* xl = win + (int)(j0 / L - (T - 1) - qa);
-    const float* row = seq + (int)((tile * kWave + lane) % C) * kCtClassStride;
+    const int jl = (int)(m0 * M + a.c) + kGenTS * M * lane;
+    const float* xl = win + (jl / L - (T - 1) - (int)qa);
+    const float* row = seq + (((int)tile * kWave + lane) % C) * kCtClassStride;
     f32x2 X[NPW];
 #pragma unroll
     for (int m = 0; m < NPW; ++m) X[m] = f32x2{xl[2 * m], xl[2 * m + 1]};
@@ -1276,7 +1291,8 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
     tp->win = 0;
     return true;
   }
-  if (L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
+  if (L == 160 && M == 147 && TT <= kGenTT && gen_classes(L, M) <= kGenClasses &&
+      (n_out + kGenTile) * M + c < ((int64_t)1 << 31)) {
     // Window pairs up to (31 M div L) rounded to even + 10 past the lane's
     // start: at most 1 float beyond gen_window's span; +4 keeps the rounding.
     const int win = gen_window(L, M, TT) + 4;
@@ -1289,7 +1305,8 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
       return true;
     }
   }
-  if (TT <= kGenTT && gen_classes(L, M) <= kGenClasses) {
+  if (TT <= kGenTT && gen_classes(L, M) <= kGenClasses &&
+      (n_out + kGenTile) * M + c < ((int64_t)1 << 31)) {
     const int win = gen_window(L, M, TT);
     if (gen_lds_bytes(win) <= kGenLdsMax) {
       tp->kind = 2;
