@@ -257,10 +257,12 @@ def valu_work(chain, mean_ms):
             "fp64_fma_per_output_sample": round(per_sample, 3),
             "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
-            "note": "beside the fp64 FMAs the kernel issues 27 (L3/M2) or 10 (generic) "
-                    "v_pk_fma_f32 per sample (SRC + pass 1); it runs at the 1400 W package "
-                    "power cap (config 4: sclk ~1.72 GHz of 2.4; a pure 1R:2W HBM stream at "
-                    "5.1 TB/s draws ~865 W), profiles/r03_power_clocks.txt, DESIGN.md §3.0.2"}
+            "note": "beside the fp64 FMAs the kernel issues 19.7 (L3/M2: SRC 656 + pass 1 288 "
+                    "per 48-sample lane sub-chunk) or 10 (generic) v_pk_fma_f32 per sample; it "
+                    "runs at the 1400 W package power cap and is VALU-issue-bound at the clock "
+                    "that leaves (config 4: 91 % of the kernel's cycles issue VALU at ~1.64 GHz, "
+                    "PMC, profiles/r04_m1_c4_pmc_summary.txt; a pure 1R:2W HBM stream at 5.1 TB/s "
+                    "draws ~865 W), DESIGN.md §3.0.2, §3.0.5"}
 
 
 def load_traffic(wl_name, channels):

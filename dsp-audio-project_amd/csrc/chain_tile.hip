@@ -280,18 +280,47 @@ typedef __attribute__((address_space(4))) const TileTables* tt_ptr;
 // pair, pairs p ascending, and y = even + odd -- the summation order of
 // k_src_reg's packed path (src_poly.hip), so y is bitwise the SRC kernel's.
 // DLY: branch 0's taps are zero but for its centre tap u = TT / 2 (the
-// host's kernel taps with the sinc-zero noise flushed, design.kernel_taps;
+// caller's taps with the sinc-zero noise flushed, common.h kTapFlushRel;
 // dsp_chain_tile_tables checks it and marks the key): its outputs, every L-th,
 // are that tap times one sample -- one multiply instead of NP packed FMAs, and
-// bitwise what the FMA chain gives on these taps (t x rounded once; the zero
-// taps add signed zeros).  Outputs of other branches are unchanged.
+// for a finite window bitwise what the FMA chain gives on these taps (t x
+// rounded once; the zero taps add signed zeros).  A window with an inf or NaN
+// (0 * inf = NaN in the chain, not here) is rerun by the repair kernel with
+// the reference's semantics (tile_cascade).  Outputs of other branches are
+// unchanged.
 template <class GEO>
 constexpr bool dly_out(int i) { return GEO::phi(i) == 0; }
+// DLY also skips the tap pairs that lie wholly outside the reference's
+// default filter (K = 40 L + 1 taps; branch 1's first pair at L3/M2): both
+// of their taps are zero in every table with the DLY key (delay_branch).
+template <class GEO>
+constexpr bool void_pair(int p, int ph) {
+  const int a = branch_parity<GEO>(ph);
+  if (a < 0) return true;
+  for (int e = 0; e < 2; ++e) {
+    const int u = 2 * p + e - a;
+    if (u >= 0 && u < GEO::TT && ph + GEO::L * (GEO::TT - 1 - u) < 40 * GEO::L + 1) return false;
+  }
+  return true;
+}
+// ... as a table, so that the unrolled SRC loops index a constant (a call
+// there was left to run time).
+struct VoidPairs {
+  bool v[kNPMax][4];
+};
+template <class GEO>
+constexpr VoidPairs void_pairs() {
+  VoidPairs t{};
+  for (int p = 0; p < kNPMax; ++p)
+    for (int ph = 0; ph < 4; ++ph) t.v[p][ph] = ph < GEO::L && p < GEO::NP && void_pair<GEO>(p, ph);
+  return t;
+}
 template <class GEO>
 constexpr int dly_slot() { return GEO::TT / 2 + (branch_parity<GEO>(0) > 0 ? 1 : 0); }
 
 template <class GEO, int H0, int NH, bool DLY = false>
 __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[GEO::TSUB]) {
+  static constexpr VoidPairs kVoid = void_pairs<GEO>();
   constexpr int V0 = GEO::qs(H0) / 4 * 4;
   constexpr int V1 = GEO::qs(H0 + NH - 1) + 2 * GEO::NP;
   constexpr int NV = (V1 - V0 + 3) / 4 * 4;
@@ -316,7 +345,7 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
     for (int ph = 0; ph < GEO::L; ++ph) t[ph] = f32x2{tq->TP[p][ph][0], tq->TP[p][ph][1]};
 #pragma unroll
     for (int i = 0; i < NH; ++i)
-      if (!(DLY && dly_out<GEO>(H0 + i)))
+      if (!(DLY && (dly_out<GEO>(H0 + i) || kVoid.v[p][GEO::phi(H0 + i)])))
         acc[i] = __builtin_elementwise_fma(t[GEO::phi(H0 + i)],
                                            w[(GEO::qs(H0 + i) - V0) / 2 + p], acc[i]);
   }
@@ -1640,6 +1669,11 @@ bool delay_branch(const TileTables* tt) {
       const bool centre = 2 * p + e == sl;
       if (centre ? !(std::isfinite(v) && v != 0.f) : v != 0.f) return false;
     }
+  // the pairs the DLY kernel skips (void_pair) hold zero taps
+  for (int p = 0; p < GEO::NP; ++p)
+    for (int ph = 1; ph < GEO::L; ++ph)
+      if (void_pair<GEO>(p, ph) && (tt->TP[p][ph][0] != 0.f || tt->TP[p][ph][1] != 0.f))
+        return false;
   return true;
 }
 
