@@ -41,6 +41,9 @@ CONFIGS = {
     "c1": (44100, 2, 1, 127, 441000, "flat", 1024, 100000, (3840, 3840)),
     "c3": (48000, 3, 2, None, 48000, "c3", 4096, None, (3072, 48)),
     "c5": (44100, 160, 147, 1023, 12000, "c3", 4096, None, (2048, 32)),
+    # the generic single-pass kernel (k_chain_gen), up- and down-sampling
+    "g54": (48000, 5, 4, 31, 9000, "c3", 2048, None, (2048, 32)),
+    "g23": (48000, 2, 3, 15, 6600, "c3", 2048, None, (2048, 32)),
 }
 FLAT = {"Sub-Bass": 0, "Bass": 0, "Low Mids": 0, "High Mids": 0, "Presence": 0, "Brilliance": 0}
 
@@ -191,7 +194,7 @@ def test_nonfinite_drop_in_matches_reference(gpu, name):
     _check(name, y, z, mag, "drop-in")
 
 
-@pytest.mark.parametrize("name", ["c3", "c5"])
+@pytest.mark.parametrize("name", ["c3", "c5", "g54"])
 def test_nonfinite_host_chain_matches_reference(gpu, name):
     """HostChain (numpy in and out, pipelined blocks of 5 rows, 2 slots)."""
     from dspcore.host import HostChain

@@ -604,10 +604,25 @@ def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
         assert np.max(np.abs(mag[b].cpu().numpy() - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
 
 
+def _all_rows_match_two_launch(ch, x):
+    """Every row of a single-pass run against the two-launch chain (SRC kernel +
+    two-pass cascade, dsp_chain_path(1)) on the same input: y bitwise, z within
+    2e-6 (include/dspcore.h), |Z| within the spectrum tolerance -- the whole
+    batch, not sampled rows."""
+    y, z, mag = (t.clone() for t in ch.run(x))
+    with _chain_path(1):
+        y2, z2, m2 = ch.run(x)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y)
+    assert float((z2 - z).abs().max()) <= 2e-6
+    assert float((m2 - mag).abs().max()) <= CHAIN_MAG_RTOL * float(mag.abs().max())
+    del y, z, mag
+
+
 def test_chain_config4_one_gpu_and_shards(gpu):
     """Config 4 on one GPU (32768 x 48000: 2.36e9 output elements, row offsets
-    past 2^31): spot rows against the oracle, including row 32767, and the
-    last shard of the 2-, 4- and 8-GPU splits (16384 / 8192 / 4096 channels,
+    past 2^31): every row against the two-launch chain, 16 rows (incl. row
+    32767) against the oracle, and the last shard of the 2-, 4- and 8-GPU splits (16384 / 8192 / 4096 channels,
     bench.py's per-rank batches) bitwise equal to the full run's rows."""
     from dspcore.chain import Chain, ChainConfig
     from dspcore.shard import shard_ranges
@@ -622,7 +637,8 @@ def test_chain_config4_one_gpu_and_shards(gpu):
     torch.cuda.synchronize()
     assert ch.handoff_ok()
     assert float(z.abs().max()) <= 1.0 and torch.isfinite(mag).all()
-    for b in (0, 16383, 16384, 32767):
+    rows = sorted({0, 16383, 16384, 32767} | set(np.random.default_rng(44).integers(0, B, 12)))
+    for b in rows:
         ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, orc.CONFIG3_GAINS,
                                        None, 4096)
         assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL
@@ -635,12 +651,15 @@ def test_chain_config4_one_gpu_and_shards(gpu):
         assert torch.equal(ys, y[lo:hi]) and torch.equal(zs, z[lo:hi]) and torch.equal(ms, mag[lo:hi])
         assert sh.handoff_ok()
         del sh, ys, zs, ms
+    del y, z, mag
+    _all_rows_match_two_launch(ch, x)
 
 
 def test_chain_config5_full_batch_and_shards(gpu):
     """Config 5 at full size on one GPU (8192 x 48000 at 44.1 kHz, L/M =
-    160/147, K = 1023: the generic single-pass kernel): spot rows against the
-    oracle on both sides of the 2-way split, and the last shard of the 2-, 4-
+    160/147, K = 1023: the generic single-pass kernel): every row against the
+    two-launch chain, 16 rows against the oracle on both sides of the 2-way
+    split, and the last shard of the 2-, 4-
     and 8-GPU splits (4096 / 2048 / 1024 channels) bitwise equal to the full
     run's rows (the kernel's arithmetic depends on L, M, K only)."""
     from dspcore.chain import Chain, ChainConfig
@@ -656,7 +675,8 @@ def test_chain_config5_full_batch_and_shards(gpu):
     torch.cuda.synchronize()
     assert ch.handoff_ok()
     assert float(z.abs().max()) <= 1.0 and torch.isfinite(mag).all()
-    for b in (0, 4095, 4096, B - 1):
+    rows = sorted({0, 4095, 4096, B - 1} | set(np.random.default_rng(55).integers(0, B, 12)))
+    for b in rows:
         ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 44100, 160, 147, orc.CONFIG3_GAINS,
                                        1023, 4096)
         assert np.max(np.abs(y[b].cpu().numpy() - ry)) <= SRC_ATOL
@@ -669,6 +689,8 @@ def test_chain_config5_full_batch_and_shards(gpu):
         assert torch.equal(ys, y[lo:hi]) and torch.equal(zs, z[lo:hi]) and torch.equal(ms, mag[lo:hi])
         assert sh.handoff_ok()
         del sh, ys, zs, ms
+    del y, z, mag
+    _all_rows_match_two_launch(ch, x)
 
 
 def test_drop_in_shards_large_batches(gpu, monkeypatch):
