@@ -45,14 +45,36 @@ def short(name):
     return None
 
 
+N_SIMD = 1024      # MI355X: 256 CUs x 4 SIMDs
+N_XCD = 8
+
+
+def pass_durations(pass_dir):
+    """Mean kernel duration (ns) per short name in one pass's kernel trace."""
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(pass_dir, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row.get("Kernel_Name", ""))
+                if k:
+                    durs[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in durs.items()}
+
+
 def main(root, write=None):
     vals = defaultdict(lambda: defaultdict(list))
+    grbm_dur = defaultdict(list)   # kernel durations (ns) of the passes that count GRBM_GUI_ACTIVE
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        has_grbm = False
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = short(row.get("Kernel_Name", ""))
                 if k:
                     vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    has_grbm = has_grbm or row["Counter_Name"] == "GRBM_GUI_ACTIVE"
+        if has_grbm:
+            for k, d in pass_durations(os.path.dirname(f)).items():
+                grbm_dur[k].append(d)
     out = {}
     for k in sorted(vals):
         c = {n: sum(v) / len(v) for n, v in vals[k].items()}
@@ -64,6 +86,23 @@ def main(root, write=None):
             t = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
             c["traffic_bytes"] = t
             print(f"   traffic (2*FETCH+WRITE)     {t / 1e9:.4f} GB per launch")
+        # effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration, MI355X_MICROARCH.md DVFS) and
+        # the share of the kernel's cycles each SIMD issues VALU (SQ_ACTIVE_INST_VALU counts
+        # quad-cycles: one per wave64 VALU instruction)
+        if "GRBM_GUI_ACTIVE" in c and grbm_dur.get(k):
+            cycles = c["GRBM_GUI_ACTIVE"] / N_XCD
+            dur = sum(grbm_dur[k]) / len(grbm_dur[k])
+            c["clock_ghz"] = cycles / dur
+            print(f"   effective clock             {c['clock_ghz']:.3f} GHz ({dur / 1e6:.4f} ms)")
+            if "SQ_ACTIVE_INST_VALU" in c:
+                c["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / cycles
+                print(f"   VALU-busy share of cycles   {c['valu_busy_frac']:.3f}")
+        if "SQ_INSTS_VALU" in c and c.get("SQ_WAVES"):
+            c["valu_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+            print(f"   VALU per wave               {c['valu_per_wave']:.1f}")
+        if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+            c["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+            print(f"   LDS bank-conflict share     {c['lds_conflict_frac']:.4f}")
     if write:
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                             "pmc_traffic.json")
@@ -74,7 +113,11 @@ def main(root, write=None):
         wl, channels, source = write
         data[wl] = {"channels": int(channels), "source": source,
                     "per_launch": {k: round(c["traffic_bytes"]) for k, c in out.items()
-                                   if "traffic_bytes" in c}}
+                                   if "traffic_bytes" in c},
+                    "derived": {k: {n: round(c[n], 4) for n in
+                                    ("clock_ghz", "valu_busy_frac", "valu_per_wave",
+                                     "lds_conflict_frac") if n in c}
+                                for k, c in out.items()}}
         with open(path, "w") as fh:
             json.dump(data, fh, indent=1)
         print("wrote", path)
