@@ -23,7 +23,8 @@ struct TraceState {
 };
 thread_local TraceState g_trace;
 // dsp_chain_path: 0 single-pass kernel where instantiated (default), 1 always
-// the two-launch chain.
+// the two-launch chain, 2 / 3 the single-pass path with its chained-tile /
+// persistent kernel (where one is built for the geometry).
 thread_local int g_chain_path = 0;
 // dsp_chain_spin_limit: polls before a single-pass hand-off wait gives up
 // (2^23 polls with s_sleep 2 between them: ~0.4 s).
@@ -74,7 +75,8 @@ int dsp_version(void) {
   // the sinc-zero noise itself (common.h, kTapFlushRel); inf and NaN input
   // propagate as through the reference's float64 convolution (round 4).
   // 2.2.0: dsp_pcm_batch_to_mono_f32 / dsp_pcm_batch_workspace_bytes (round 4).
-  return 20200;
+  // 2.3.0: dsp_chain_path 2 / 3 pick the single-pass kernel variant (round 4).
+  return 20300;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
@@ -154,7 +156,7 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_
 
 int dsp_chain_path(int32_t path) {
   dsp::clear_error();
-  if (path < -1 || path > 1) return dsp::set_error(DSP_EINVAL, "chain path %d not in [-1, 1]", path);
+  if (path < -1 || path > 3) return dsp::set_error(DSP_EINVAL, "chain path %d not in [-1, 3]", path);
   const int prev = dsp::g_chain_path;
   if (path >= 0) dsp::g_chain_path = path;
   return prev;
@@ -232,10 +234,11 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
               "chain workspace too small: %zu < %zu bytes (dsp_chain_workspace_bytes)",
               workspace_bytes, head);
   int rc = dsp::kNotFused;
-  if (dsp::g_chain_path == 0)
+  if (dsp::g_chain_path != 1)
     rc = dsp::launch_chain_tile(x, y, z, B, n_in, ld_x, n_out, ld_y, taps, K, L, M, c_offset,
                                 sos_host, S, clip, tile_tables, tile_key,
-                                (uint32_t)dsp::g_spin_limit, workspace, head, s);
+                                (uint32_t)dsp::g_spin_limit, dsp::g_chain_path, workspace, head,
+                                s);
   if (rc == dsp::kNotFused) {
     // Two-launch chain: SRC, then the cascade with x-domain chunk states where
     // the input rows are aligned and the chunking fits, else the y-domain

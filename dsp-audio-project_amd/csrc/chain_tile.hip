@@ -77,6 +77,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "cascade.h"
 
@@ -635,10 +636,21 @@ __device__ __forceinline__ void fix_outputs(const TileArgs& a, tt_ptr mt, int64_
 // reruns pass 1 on the fixed y and makes E' NaN for a lane whose y holds an
 // inf or NaN (as nf_poison: every later output of the channel is NaN, as in
 // the reference's cascade).
-template <int TS, bool YST = true, bool REPAIR = false, class ONNF>
+// Where a tile's entry state comes from.  ChainedEntry: the previous tile's
+// workgroup (the hand-off above).  RegCarry (persistent kernels, which run the
+// tiles of a channel in order in one wave): registers -- the previous tile's
+// end state as its scan left it, block kb of it in each worker lane of
+// segment 7 (tile_cascade stores it to the park row and refreshes it).
+struct ChainedEntry {};
+struct RegCarry {
+  double c0, c1;
+};
+
+template <int TS, bool YST = true, bool REPAIR = false, class ONNF, class ENTRY = ChainedEntry>
 __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
                                              float (&y)[TS], int lane, int64_t b, int64_t tile,
-                                             int64_t m0, ONNF&& on_nf) {
+                                             int64_t m0, ONNF&& on_nf, ENTRY&& entry = ENTRY{}) {
+  constexpr bool kRegCarry = std::is_same_v<std::decay_t<ENTRY>, RegCarry>;
   // ---- 2. pass 1: zero-state end state of the sub-chunk
   double v[kD];
   pass1_state<TS>(mt, y, v);
@@ -676,6 +688,11 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
 #pragma unroll
       for (int k = 0; k < kS; ++k) *reinterpret_cast<f64x2*>(park + 2 * k) = f64x2{0.0, 0.0};
     }
+  } else if constexpr (kRegCarry) {
+    // segment 7's lanes hold the previous tile's end state, block lane & 7
+    // (lanes 62, 63: the park row's unused slots 12..15)
+    if ((lane >> 3) == 7)
+      *reinterpret_cast<f64x2*>(park + 2 * (lane & 7)) = f64x2{entry.c0, entry.c1};
   } else {
     double m_in[kD];
     tile_entry_state(a, b, tile, lane, m_in);
@@ -699,7 +716,7 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // rows, in bounds, never used for a stored value)
   const int kb = lane & 7;
   const __attribute__((address_space(1))) double* Dg =
-      (const __attribute__((address_space(1))) double*)&a.tt->Dp[0][kb][0];
+      (const __attribute__((address_space(1))) double*)&mt->Dp[0][kb][0];
   const f64x2 d0a = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg);
   const f64x2 d0b = *reinterpret_cast<const __attribute__((address_space(1))) f64x2*>(Dg + 2);
   f64x2 e[8];
@@ -769,7 +786,10 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
       store_state(a.states + me * kD + 2 * kb, u0);
       store_state(a.states + me * kD + 2 * kb + 1, u1);
     }
-    if (tile + 1 < a.ntiles) {
+    if constexpr (kRegCarry) {
+      entry.c0 = u0;
+      entry.c1 = u1;
+    } else if (tile + 1 < a.ntiles) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 8 * 7) store_flag(a.flags + me, 1u);
     }
@@ -1170,25 +1190,31 @@ __device__ __forceinline__ void ct_load_classes(const TileArgs& a, float* seq) {
   __syncthreads();
 }
 
-// One tile of k_chain_gct for one wave (REPAIR: the rerun with the
-// non-finite path).
-template <int L, int M, bool T7, bool REPAIR>
-__device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* seq, float* win,
-                                               int lane, int64_t b, int64_t tile) {
+// x offset (a multiple of 4) of the x window of a generic kernel's tile.
+template <int L, int M>
+__device__ __forceinline__ int64_t gen_window_start(const TileArgs& a, int64_t tile) {
+  const int64_t qlo = (tile * kGenTile * M + a.c) / L - (a.T - 1);
+  return (qlo >> 2) << 2;
+}
+
+// Steps 1-5 of one tile of k_chain_gct for one wave whose x window x[qa ..]
+// is in `win` (REPAIR: the rerun with the non-finite path; entry:
+// tile_cascade's).
+template <int L, int M, bool T7, bool REPAIR, class ENTRY = ChainedEntry>
+__device__ __forceinline__ void gct_tile(const TileArgs& a, const float* seq, float* win,
+                                         int lane, int64_t b, int64_t tile, int64_t qa,
+                                         ENTRY&& entry = ENTRY{}) {
   static_assert(M < L, "q advances by 0 or 1 per output");
   constexpr int NPW = ((kGenTS - 1) * M / L) / 2 + kCtTaps / 2;  // window pairs per lane
   const int T = a.T;
-  const tt_ptr mt = (tt_ptr)a.tt;
+  // (opaque: in the persistent kernel's tile loop, table loads stay where
+  // they are used instead of hoisted out of the loop into live registers)
+  tt_ptr mt = (tt_ptr)a.tt;
+  asm volatile("" : "+s"(mt));
   // the phase classes of the 32-output sub-chunk starts, known at compile
   // time for the ratio (gen_classes; the host checked the tables hold as many)
   constexpr int C = L / ct_gcd((kGenTS * M) % L, L);
   const int64_t m0 = tile * kGenTile;
-
-  // ---- x window of the tile
-  const int64_t qlo = (m0 * M + a.c) / L - (T - 1);
-  const int64_t qa = (qlo >> 2) << 2;
-  gen_load_window(a, win, lane, b, qa);
-  fence();
 
   // ---- 1. SRC of the lane's 32 outputs from its register window
   // (j = m M + c in 32 bits: tile_geometry keeps n_out M + c below 2^31)
@@ -1226,7 +1252,17 @@ __device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* s
                                        gen_fix(a, mt, win, qa, j0, b, m0 + kGenTS * lane, yy, v);
                                      });
   else
-    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0);
+    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0, entry);
+}
+
+// One tile of k_chain_gct for one wave: its x window, then gct_tile.
+template <int L, int M, bool T7, bool REPAIR>
+__device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* seq, float* win,
+                                               int lane, int64_t b, int64_t tile) {
+  const int64_t qa = gen_window_start<L, M>(a, tile);
+  gen_load_window(a, win, lane, b, qa);
+  fence();
+  gct_tile<L, M, T7, REPAIR>(a, seq, win, lane, b, tile, qa);
 }
 
 template <int L, int M, bool T7 = false>
@@ -1256,6 +1292,57 @@ __global__ __launch_bounds__(kWave * kGenWaves) void k_chain_gct_repair(TileArgs
   repair_channels(a, w, kGenWaves, [&](int64_t b, int64_t tile) {
     chain_gct_body<L, M, T7, true>(a, seq, win, lane, b, tile);
   });
+}
+
+// Persistent k_chain_gct (round 4), for batches of at least a chip's worth of
+// workgroups: a workgroup loads the class rows once and walks channel groups
+// (grid-stride); each wave runs its channel's tiles in order, carrying the
+// end state in registers (RegCarry: no hand-off, no flags, no tile waiting on
+// another workgroup).  Every tile's end state is still published for the
+// repair kernel.  Rows are bitwise the chained kernel's: the same tile code on
+// the same entry states.  Config 5 (8192 channels): 1.134-1.137 vs
+// 1.191-1.200 ms same box (profiles/r04_gcp_ab.txt).  Issuing part of the next
+// tile's window behind pass 2 (registers) measured the same with 2 of its 8
+// float4 per lane and slower with 4 (spills): not kept.
+constexpr int kGcpWin = 8;  // float4 per lane of a tile's x window (a.win <= 4 * 8 * 64)
+
+template <int L, int M, bool T7 = false>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gcp(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
+  float* seq = smem;
+  ct_load_classes(a, seq);
+  float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
+  const int nf = a.win >> 2;
+  for (int64_t g = blockIdx.x; g < groups; g += gridDim.x) {
+    const int64_t b = g * kGenWaves + w;
+    if (b >= a.B) break;  // the last group's missing channels (wave-uniform)
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    RegCarry carry{0.0, 0.0};
+    for (int64_t tile = 0; tile < a.ntiles; ++tile) {
+      const int64_t qa = gen_window_start<L, M>(a, tile);
+      f32x4 v[kGcpWin];
+#pragma unroll
+      for (int r = 0; r < kGcpWin; ++r)  // past the window: harmless reads
+        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * (r * kWave + lane)) * 4),
+                                                     0, kStream);
+#pragma unroll
+      for (int r = 0; r < kGcpWin; ++r) {
+        const int f = r * kWave + lane;
+        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+      }
+      fence();
+      // (an opaque lane per tile: what the tile derives from it is recomputed
+      // instead of hoisted out of the loop and held through it)
+      int ln = lane_id();
+      asm volatile("" : "+v"(ln));
+      gct_tile<L, M, T7, false>(a, seq, win, ln, b, tile, qa, carry);
+    }
+  }
 }
 
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
@@ -1764,7 +1851,8 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
                       int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
                       int64_t c, const double* sos, int S, int clip, const void* tables,
-                      uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s) {
+                      uint64_t key, uint32_t max_spins, int variant, void* ws, size_t ws_bytes,
+                      hipStream_t s) {
   TilePlan tp;
   if (!tables || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return kNotFused;
   DSP_REQUIRE(taps, "null taps");  // the non-finite path reads the caller's taps
@@ -1831,12 +1919,26 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const size_t shm = ct_lds_bytes(gen_classes(L, M), tp.win);
     auto kern = a.T <= 7 ? k_chain_gct<160, 147, true> : k_chain_gct<160, 147, false>;
     auto rep = a.T <= 7 ? k_chain_gct_repair<160, 147, true> : k_chain_gct_repair<160, 147, false>;
+    auto pers = a.T <= 7 ? k_chain_gcp<160, 147, true> : k_chain_gcp<160, 147, false>;
     if (int rc = allow_lds(kern, shm)) return rc;
     if (int rc = allow_lds(rep, shm)) return rc;
+    if (int rc = allow_lds(pers, shm)) return rc;
+    // Persistent kernel when the batch fills the chip with whole rounds of
+    // channel groups (a smaller batch runs the chained kernel, whose tiles of
+    // one channel overlap everything but their carry).
+    const int res = a.T <= 7 ? resident_groups<k_chain_gcp<160, 147, true>>(kWave * kGenWaves, shm)
+                             : resident_groups<k_chain_gcp<160, 147, false>>(kWave * kGenWaves, shm);
+    const int64_t rounds = res > 0 ? ceil_div(groups, res) : 0;
+    const bool persistent = tp.win <= 4 * kGcpWin * kWave && res > 0 && groups >= res &&
+                            groups * 8 >= rounds * res * 7 && variant != 2;
     {
       TraceScope trace("chain_tile", s);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
-                         s, a);
+      if (persistent || (variant == 3 && tp.win <= 4 * kGcpWin * kWave))
+        hipLaunchKernelGGL(pers, dim3((unsigned)std::min<int64_t>(groups, std::max(res, 1))),
+                           dim3(kWave * kGenWaves), shm, s, a);
+      else
+        hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves),
+                           shm, s, a);
     }
     TraceScope trace("chain_repair", s);
     hipLaunchKernelGGL(rep, dim3(rgrid), dim3(kWave * kGenWaves), shm, s, a);

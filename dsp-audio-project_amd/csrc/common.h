@@ -79,6 +79,27 @@ inline int allow_lds(Kern kernel, size_t bytes) {
   return DSP_OK;
 }
 
+// Resident workgroups on the device for a kernel (asked once per calling thread and
+// kernel instance; thread_local: no state shared between threads).  The
+// kernel is a template argument so that every kernel has its own cache (as a
+// function argument, every instance of one signature shared it).
+template <auto K>
+int resident_groups(int threads, size_t shm) {
+  thread_local int dev = -1, cached = 0;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  if (d != dev || cached <= 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K),
+                                                     threads, shm) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      return 0;
+    dev = d;
+    cached = per_cu * cus;
+  }
+  return cached;
+}
+
 // Workgroup barrier that waits only for LDS traffic.  __syncthreads() also
 // drains outstanding global loads/stores (vmcnt(0)) on gfx950, which would
 // serialise prefetches and stores with the barrier.
@@ -244,13 +265,15 @@ size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K,
 size_t chain_tile_tables_bytes();
 int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, const float* taps,
                       int K, int L, int M, int64_t c, const double* sos, int S, uint64_t* key);
-// y may be NULL (the y store is skipped).  Returns kNotFused (nothing
+// y may be NULL (the y store is skipped).  variant: dsp_chain_path's setting
+// (0 the launcher's choice, 2 chained tiles, 3 persistent).  Returns kNotFused (nothing
 // launched) when the kernel does not serve the call or `key` is not the
 // fingerprint of tables built for it.
 int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_in, int64_t ld_x,
                       int64_t n_out, int64_t ld_y, const float* taps, int K, int L, int M,
                       int64_t c, const double* sos, int S, int clip, const void* tables,
-                      uint64_t key, uint32_t max_spins, void* ws, size_t ws_bytes, hipStream_t s);
+                      uint64_t key, uint32_t max_spins, int variant, void* ws, size_t ws_bytes,
+                      hipStream_t s);
 // Whether launch_biquad_xstate's conditions on the cascade (n, S, chunk_len)
 // and on the SRC input rows (16-byte aligned) hold.
 bool xstate_applicable(int64_t n, int S, int64_t chunk_len, const float* xs, int64_t ld_xs,

@@ -617,27 +617,6 @@ __attribute__((amdgpu_waves_per_eu(kSpecWaves))) void k_spec_stream(FftArgs a, i
   }
 }
 
-// Resident workgroups per CU for a kernel (asked once per calling thread and
-// kernel instance; thread_local: no state shared between threads).  The
-// kernel is a template argument so that every kernel has its own cache (as a
-// function argument, every instance of one signature shared it).
-template <auto K>
-int resident_groups(int threads, size_t shm) {
-  thread_local int dev = -1, cached = 0;
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess) return 0;
-  if (d != dev || cached <= 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K),
-                                                     threads, shm) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      return 0;
-    dev = d;
-    cached = per_cu * cus;
-  }
-  return cached;
-}
-
 template <int LOG2N>
 int launch_spec_stream(const FftArgs& a, hipStream_t s) {
   using PL = Plan<LOG2N - 1>;

@@ -162,7 +162,9 @@ def check(rc: int, what: str) -> None:
 def chain_path(path: int = -1) -> int:
     """Path of dsp_chain_f32 on the calling thread (dsp_chain_path): 0 the
     single-pass kernel where it applies (default), 1 always the two-launch
-    chain; -1 only queries.  Returns the previous setting."""
+    chain, 2 / 3 the single-pass path with its chained-tile / persistent
+    kernel (include/dspcore.h); -1 only queries.  Returns the previous
+    setting."""
     rc = load().dsp_chain_path(int(path))
     if rc < 0:
         check(rc, "dsp_chain_path")

@@ -249,8 +249,13 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * dsp_biquad_cascade_f32.
  *
  * dsp_chain_path sets the path for the calling thread: 0 (default) the
- * single-pass kernel where it applies, 1 always the two-launch chain; -1 only
- * queries; returns the previous setting (DSP_EINVAL for anything else).
+ * single-pass kernel where it applies, 1 always the two-launch chain, 2 the
+ * single-pass path with chained tiles only (one workgroup per tile, the
+ * hand-off above), 3 the single-pass path with its persistent kernel where
+ * one is built (L/M = 160/147: each wave runs its channels' tiles in order,
+ * the entry state in registers; the default picks it for batches that fill
+ * the chip); -1 only queries; returns the previous setting (DSP_EINVAL for
+ * anything else).  Every variant gives bitwise the same y and z.
  * ------------------------------------------------------------------------- */
 int dsp_chain_path(int32_t path);
 int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,

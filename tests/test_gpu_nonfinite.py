@@ -180,6 +180,25 @@ def test_nonfinite_chain_paths_match_reference(gpu, name):
     np.testing.assert_array_equal(y[fin], y2[fin])
 
 
+def test_nonfinite_persistent_kernel_matches_reference(gpu):
+    """Config 5's persistent single-pass kernel (dsp_chain_path(3): each wave
+    runs its channels' tiles in order, the entry state in registers), then the
+    repair kernel: the oracle's masks, and y and z bitwise the chained-tile
+    kernel's (dsp_chain_path(2))."""
+    from dspcore.chain import Chain
+    x, _, _ = _case("c5")
+    ch = Chain(_cfg("c5"), x.shape[0], gpu)
+    xd = torch.from_numpy(x).to(gpu)
+    with _chain_path(3):
+        y, z, mag = (t.cpu().numpy() for t in ch.run(xd))
+    _check("c5", y, z, mag, "persistent")
+    with _chain_path(2):
+        y2, z2, m2 = (t.cpu().numpy() for t in ch.run(xd))
+    np.testing.assert_array_equal(y, y2)
+    np.testing.assert_array_equal(z, z2)
+    np.testing.assert_array_equal(mag, m2)
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_nonfinite_drop_in_matches_reference(gpu, name):
     """The drop-in module's calls, as app.py makes them, on the [B, n] batch."""

@@ -557,6 +557,39 @@ def test_chain_generic_single_pass(gpu, n_in, fs, L, M, K, B):
                  gpu).tile_len == 0
 
 
+@pytest.mark.parametrize("B,n_in", [(1, 48000), (5, 48000), (9, 12000), (16, 4800)])
+def test_chain_config5_persistent_bitwise_chained(gpu, B, n_in):
+    """Config 5's ratio (160/147, K = 1023) through the persistent single-pass
+    kernel (dsp_chain_path(3): a workgroup walks channel groups, each wave runs
+    its channel's tiles in order with the entry state in registers and the next
+    window in flight) and through the chained-tile kernel (dsp_chain_path(2)):
+    y, z and |X| bitwise equal (same tile code on the same entry states), for
+    partial channel groups and ragged last tiles; both match the oracle."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    n_fft = 4096 if n_in >= 10000 else 2048
+    cfg = ChainConfig(n_in, 44100, 160, 147, 1023, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 32
+    gen = torch.Generator(device=gpu).manual_seed(21)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[B - 1] *= 30.0                   # drive the clip
+    with _chain_path(3):
+        (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
+    with _chain_path(2):
+        (y0, z0, m0), names0 = _traced(lambda: ch.run(x))
+    assert "chain_tile" in names1 and "chain_tile" in names0, (names1, names0)
+    assert ch.handoff_ok()
+    assert torch.equal(y1, y0) and torch.equal(z1, z0) and torch.equal(m1, m0)
+    y, z, mag = (t.cpu().numpy() for t in (y1, z1, m1))
+    for b in sorted({0, B - 1}):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 44100, 160, 147, orc.CONFIG3_GAINS,
+                                       1023, n_fft)
+        assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+
+
 @pytest.mark.parametrize("gains", [{"Sub-Bass": 6, "Bass": 0.0, "Presence": -3, "Otra": 4},
                                    {"Sub-Bass": 0, "Bass": 0.05}])
 def test_chain_single_pass_fewer_bands_and_bypass(gpu, gains):

@@ -35,6 +35,8 @@ def run(args):
         _chain.caller_taps = _design.caller_taps = _flushed
 
     os.makedirs(OUT, exist_ok=True)
+    if args.path is not None:
+        _lib.chain_path(args.path)          # dsp_chain_path: kernel variant
     wl = dict(WORKLOADS[args.config])
     dev = torch.device("cuda", 0)
     cfg = ChainConfig(wl["n_in"], wl["fs"], wl["L"], wl["M"], wl["num_taps"], CONFIG3_GAINS,
@@ -96,6 +98,7 @@ if __name__ == "__main__":
     ap.add_argument("--channels", type=int, nargs="+", default=[4096, 32768])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--compare", nargs=2)
+    ap.add_argument("--path", type=int, default=None, help="dsp_chain_path for the run")
     args = ap.parse_args()
     if args.compare:
         compare(*args.compare)
