@@ -1906,6 +1906,8 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   const unsigned rgrid =
       (unsigned)std::min<int64_t>(ceil_div(B, kWave * rwaves), kRepairGroups);
   if (tp.kind == 1) {
+    // (No persistent variant: one measured 9 % slower at config 4 and 5 % at
+    // config 3 than these chained tiles, profiles/r04_tilep_ab.txt.)
     {
       TraceScope trace("chain_tile", s);
       auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
