@@ -947,8 +947,8 @@ template <class GEO, bool DLY = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
-  const int64_t id = blockIdx.x;
-  const int64_t tile = id / a.B, b = id - tile * a.B;  // tile-major
+  // grid (B, ntiles): linear ids tile-major (x fastest), no division
+  const int64_t tile = blockIdx.y, b = blockIdx.x;
   chain_tile_body<GEO, DLY, false>(a, lds, threadIdx.x, b, tile);
 }
 
@@ -1135,9 +1135,8 @@ k_chain_gen(TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = gen_wave();
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
-  const int64_t tile = blockIdx.x / groups;
-  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  const int64_t tile = blockIdx.y;  // grid (groups, ntiles): tile-major
+  const int64_t b = (int64_t)blockIdx.x * kGenWaves + w;
   float* seq = smem;
   uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
   gen_load_classes(a, seq, adv);
@@ -1271,9 +1270,8 @@ k_chain_gct(TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = gen_wave();
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
-  const int64_t tile = blockIdx.x / groups;
-  const int64_t b = (blockIdx.x - tile * groups) * kGenWaves + w;
+  const int64_t tile = blockIdx.y;  // grid (groups, ntiles): tile-major
+  const int64_t b = (int64_t)blockIdx.x * kGenWaves + w;
   float* seq = smem;
   ct_load_classes(a, seq);
   if (b >= a.B) return;
@@ -1332,8 +1330,10 @@ k_chain_gcp(TileArgs a) {
                                                      0, kStream);
 #pragma unroll
       for (int r = 0; r < kGcpWin; ++r) {
+        // (rows r < kGcpWin - 1 are whole: the launcher checks nf; one exec
+        // mask instead of eight held through the loop)
         const int f = r * kWave + lane;
-        if (f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+        if (r < kGcpWin - 1 || f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
       }
       fence();
       // (an opaque lane per tile: what the tile derives from it is recomputed
@@ -1390,8 +1390,21 @@ size_t ct_lds_bytes(int classes, int win) {
   return ((size_t)classes * kCtClassStride + (size_t)kGenWaves * win) * sizeof(float);
 }
 
+bool tile_geometry_any(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
+                       TilePlan* tp);
+
+// The single-pass kernels' grids are (channels or channel groups, tiles): at
+// most 65535 tiles per row (201 M outputs of the L3/M2 kernel, 134 M of the
+// generic ones); longer rows take the two-launch chain.
+constexpr int64_t kMaxTiles = 65535;
+
 bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
                    TilePlan* tp) {
+  return tile_geometry_any(n_in, n_out, K, L, M, c, S, tp) && tp->ntiles <= kMaxTiles;
+}
+
+bool tile_geometry_any(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
+                       TilePlan* tp) {
   if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
   if (L == 1 && M == 1) return false;  // SRC bypass: the caller's cascade path
   if (n_in * 4 + 16 >= ((int64_t)1 << 31) || n_out * 4 + 16 >= ((int64_t)1 << 31)) return false;
@@ -1911,7 +1924,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     {
       TraceScope trace("chain_tile", s);
       auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
-      hipLaunchKernelGGL(kern, dim3((unsigned)(B * tp.ntiles)), dim3(kWave), 0, s, a);
+      hipLaunchKernelGGL(kern, dim3((unsigned)B, (unsigned)tp.ntiles), dim3(kWave), 0, s, a);
     }
     TraceScope trace("chain_repair", s);
     auto rep = dly ? k_chain_tile_repair<Geo3241, true> : k_chain_tile_repair<Geo3241, false>;
@@ -1931,15 +1944,16 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const int res = a.T <= 7 ? resident_groups<k_chain_gcp<160, 147, true>>(kWave * kGenWaves, shm)
                              : resident_groups<k_chain_gcp<160, 147, false>>(kWave * kGenWaves, shm);
     const int64_t rounds = res > 0 ? ceil_div(groups, res) : 0;
-    const bool persistent = tp.win <= 4 * kGcpWin * kWave && res > 0 && groups >= res &&
+    const bool fits = tp.win <= 4 * kGcpWin * kWave && tp.win > 4 * (kGcpWin - 1) * kWave;
+    const bool persistent = fits && res > 0 && groups >= res &&
                             groups * 8 >= rounds * res * 7 && variant != 2;
     {
       TraceScope trace("chain_tile", s);
-      if (persistent || (variant == 3 && tp.win <= 4 * kGcpWin * kWave))
+      if (persistent || (variant == 3 && fits))
         hipLaunchKernelGGL(pers, dim3((unsigned)std::min<int64_t>(groups, std::max(res, 1))),
                            dim3(kWave * kGenWaves), shm, s, a);
       else
-        hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves),
+        hipLaunchKernelGGL(kern, dim3((unsigned)groups, (unsigned)tp.ntiles), dim3(kWave * kGenWaves),
                            shm, s, a);
     }
     TraceScope trace("chain_repair", s);
@@ -1953,7 +1967,7 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     if (int rc = allow_lds(rep, shm)) return rc;
     {
       TraceScope trace("chain_tile", s);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(groups * tp.ntiles)), dim3(kWave * kGenWaves), shm,
+      hipLaunchKernelGGL(kern, dim3((unsigned)groups, (unsigned)tp.ntiles), dim3(kWave * kGenWaves), shm,
                          s, a);
     }
     TraceScope trace("chain_repair", s);
