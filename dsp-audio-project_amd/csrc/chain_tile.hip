@@ -367,18 +367,31 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
   }
 }
 
-// Row (g div TS) of output float g = 4 (lane + 64 k) in store_tile's staging.
+// LDS float of output float g = 4 (lane + 64 k) in store_tile's staging,
+// g + 4 (g div TS) (row stride TS + 4), as a per-lane base plus a constant:
+//   TS = 32: 4 lane + 4 (lane >> 3) + 288 k (one base);
+//   TS = 48: (lane + 64 k) div 12 = a + [k >= 3] + [r + 4 (k mod 3) >= 12]
+//            with lane = 12 a + r, so three bases, by k mod 3, and 276 k + 4 [k >= 3].
 template <int TS>
-__device__ __forceinline__ int stage_row(int lane, int k) {
-  if constexpr (TS == 32) {
-    return (lane >> 3) + 8 * k;                       // (lane + 64 k) div 8
-  } else {
-    static_assert(TS == 48, "staging rows of 8 or 12 float4s");
-    // (lane + 64 k) div 12 = 5 k + (lane + 4 k) div 12, and v div 12 = (43 v) >> 9
-    // for v < 131 (lane + 4 k < 88)
-    return 5 * k + (((lane + 4 * k) * 43) >> 9);
+struct StageBase {
+  int b[3];
+  __device__ __forceinline__ explicit StageBase(int lane) {
+    if constexpr (TS == 32) {
+      b[0] = 4 * lane + 4 * (lane >> 3);
+    } else {
+      static_assert(TS == 48, "staging rows of 8 or 12 float4s");
+      const int a = (lane * 43) >> 9;  // lane div 12 (lane < 64)
+      const int r = lane - 12 * a;
+      b[0] = 4 * lane + 4 * a;
+      b[1] = b[0] + 4 * ((r + 8) >> 4);   // + 4 [r >= 8]
+      b[2] = b[0] + 4 * ((r + 12) >> 4);  // + 4 [r >= 4]
+    }
   }
-}
+  __device__ __forceinline__ int at(int k) const {
+    if constexpr (TS == 32) return b[0] + 288 * k;
+    else return b[k % 3] + 276 * k + (k >= 3 ? 4 : 0);
+  }
+};
 
 // Stores the tile's 64 x TS outputs (lane l holds outputs l*TS + i) as
 // coalesced float4s through `rs`, a buffer resource whose base is the tile's
@@ -397,6 +410,7 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
   constexpr int NF4 = (kWave / 2) * TS / 4;
   static_assert(NF4 % kWave == 0, "whole float4 rounds per half");
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const StageBase<TS> sb(lane);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     fence();
@@ -411,9 +425,9 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
 #pragma unroll
     for (int k = 0; k < NF4 / kWave; ++k) {
       // output float g = 4 (lane + 64 k) sits in row r = g div TS at r RS + g
-      // mod TS = g + 4 r; r from a multiply-shift (no 32-bit division)
+      // mod TS = g + 4 r (StageBase)
       const int g = 4 * (lane + kWave * k);
-      const float4 f = *reinterpret_cast<const float4*>(lds + g + 4 * stage_row<TS>(lane, k));
+      const float4 f = *reinterpret_cast<const float4*>(lds + sb.at(k));
       u32x4 d;
       d.x = __float_as_uint(f.x);
       d.y = __float_as_uint(f.y);
