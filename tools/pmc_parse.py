@@ -21,7 +21,7 @@ def short(name):
         return "chain_repair"
     if "k_pcm_batch" in name or "k_scale_batch" in name:
         return "pcm_batch"
-    if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gct" in name:
+    if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gc" in name:
         return "chain_tile"
     if "k_tile_prep" in name:
         return "chain_prep"
