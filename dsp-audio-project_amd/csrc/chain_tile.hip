@@ -1359,7 +1359,6 @@ k_chain_gcp(TileArgs a) {
   }
 }
 
-
 // Instantiated geometries: (L, M, ceil(K/L), c mod L).  (3, 2, 41, 0) is the
 // benchmark's L3/M2 with the default K = 121 (configs 3 and 4).
 typedef TileGeo<3, 2, 41, 0> Geo3241;
