@@ -88,6 +88,7 @@ namespace {
 // is touched once per launch).  Measured -1.6 % chain time at config 4, and
 // the spectrum launch that follows runs 6 % faster.
 constexpr int kStream = 2;
+constexpr int kSc1 = 16;  // cache policy sc1: coherent at agent scope
 constexpr int kLS = 32;  // SRC input samples per sub-chunk = lane stride in x
 constexpr int kS = 6;    // stages (fewer are padded with exact identity stages)
 constexpr int kD = 2 * kS;
@@ -659,12 +660,21 @@ struct ChainedEntry {};
 struct RegCarry {
   double c0, c1;
 };
+// k_chain_tile: the hand-off flag was polled when the tile started and, if
+// it was already raised, the state went into the LDS slot `slot` by an
+// agent-scope LDS-DMA behind the SRC and pass 1 (chain_tile_body); else the
+// chained wait as above.
+struct EarlyEntry {
+  bool early;
+  const double* slot;
+};
 
 template <int TS, bool YST = true, bool REPAIR = false, class ONNF, class ENTRY = ChainedEntry>
 __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float* lds,
                                              float (&y)[TS], int lane, int64_t b, int64_t tile,
                                              int64_t m0, ONNF&& on_nf, ENTRY&& entry = ENTRY{}) {
   constexpr bool kRegCarry = std::is_same_v<std::decay_t<ENTRY>, RegCarry>;
+  constexpr bool kEarly = std::is_same_v<std::decay_t<ENTRY>, EarlyEntry>;
   // ---- 2. pass 1: zero-state end state of the sub-chunk
   double v[kD];
   pass1_state<TS>(mt, y, v);
@@ -708,11 +718,29 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     if ((lane >> 3) == 7)
       *reinterpret_cast<f64x2*>(park + 2 * (lane & 7)) = f64x2{entry.c0, entry.c1};
   } else {
-    double m_in[kD];
-    tile_entry_state(a, b, tile, lane, m_in);
-    if (lane == 0) {
+    bool got = false;
+    if constexpr (kEarly) {
+      if (entry.early) {
+        // the state is in the LDS slot once the wave's only vector memory
+        // operation in flight, the LDS-DMA, is done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
 #pragma unroll
-      for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+          for (int k = 0; k < kS; ++k)
+            *reinterpret_cast<f64x2*>(park + 2 * k) =
+                *reinterpret_cast<const f64x2*>(entry.slot + 2 * k);
+          store_flag(a.flags + b * a.ntiles + tile - 1, 0u);  // consumed
+        }
+        got = true;
+      }
+    }
+    if (!got) {
+      double m_in[kD];
+      tile_entry_state(a, b, tile, lane, m_in);
+      if (lane == 0) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) park[d] = m_in[d];
+      }
     }
   }
   fence();
@@ -803,11 +831,15 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     if constexpr (kRegCarry) {
       entry.c0 = u0;
       entry.c1 = u1;
-    } else if (tile + 1 < a.ntiles) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 8 * 7) store_flag(a.flags + me, 1u);
     }
   }
+  // The flag follows once these state stores are acknowledged; the y stores
+  // below go out first, so that the wave does not sit in vmcnt(0) on the
+  // stores' round trip (round 4): the wait counts the y stores as younger.
+  const bool raise = !kRegCarry && tile + 1 < a.ntiles;
+  auto raise_flag = [&] {
+    if (lane == 8 * 7) store_flag(a.flags + b * a.ntiles + tile, 1u);
+  };
   fence();
   double m[kD];
   {
@@ -829,6 +861,14 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
         a.y + b * a.ld_y + m0, 0, (int)((a.n_out - m0) * 4), 0x00020000);
     store_tile<TS>(lds, y, lane, ry);
+    if (raise) {
+      // every store but store_tile's TS / 4 (two halves of TS / 8) is done
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TS / 4) : "memory");
+      raise_flag();
+    }
+  } else if (raise) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raise_flag();
   }
   pin(y);
   pass2_cascade<TS, REPAIR>(a, mt, y, m);
@@ -899,6 +939,15 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
   const int64_t m0 = tile * GEO::TILE;  // first output of the tile
   const tt_ptr mt = (tt_ptr)a.tt;       // wave-uniform: scalar loads
 
+  // Early hand-off (not in the repair rerun): lane 0 polls the previous
+  // tile's flag once now, ahead of the x window loads; if it is raised, the
+  // state follows by an agent-scope (sc1) LDS-DMA into the slot after the
+  // window -- issued after the poll returned, as the hand-off protocol
+  // requires -- and arrives behind the SRC and pass 1 instead of two global
+  // round trips after them.  Otherwise tile_cascade waits as before.
+  uint32_t fl = 0;
+  if (!REPAIR && tile > 0 && lane == 0) fl = load_flag(a.flags + b * a.ntiles + tile - 1);
+
   // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
   {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -921,6 +970,17 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
     static_assert(xpad(4 * (kWave + 7)) - xpad(4 * 7) == 288, "xpad: 288 floats per 64 float4s");
   }
   fence();  // one wave: its LDS operations execute in order
+  EarlyEntry early{false, reinterpret_cast<const double*>(lds + GEO::LDSF)};
+  if (!REPAIR && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
+    early.early = true;
+    if (lane < 2 * kD) {
+      const int64_t prev = b * a.ntiles + tile - 1;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint32_t*>(
+                                                               a.states + prev * kD) + lane),
+          (__attribute__((address_space(3))) void*)(lds + GEO::LDSF), 4, 0, kSc1);
+    }
+  }
 
   // ---- 1. SRC: the lane's TSUB outputs, in parts (register pressure)
   float y[TS];
@@ -953,14 +1013,14 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
     };
     tile_cascade<TS, true, true>(a, mt, lds, y, lane, b, tile, m0, fix);
   } else {
-    tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0);
+    tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0, early);
   }
 }
 
 template <class GEO, bool DLY = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile(
     TileArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF + 2 * kD];  // + the early slot
   // grid (B, ntiles): linear ids tile-major (x fastest), no division
   const int64_t tile = blockIdx.y, b = blockIdx.x;
   chain_tile_body<GEO, DLY, false>(a, lds, threadIdx.x, b, tile);
@@ -968,7 +1028,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 
 template <class GEO, bool DLY = false>
 __global__ __launch_bounds__(kWave) void k_chain_tile_repair(TileArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF + 2 * kD];  // + the early slot
   repair_channels(a, 0, 1, [&](int64_t b, int64_t tile) {
     chain_tile_body<GEO, DLY, true>(a, lds, (int)threadIdx.x, b, tile);
   });
