@@ -65,7 +65,12 @@
 // atomics do not need and which measured 5.8x slower (config 4: 37.7 vs
 // 6.55 ms, profiles/r03_handoff_fence_ab.txt).  The consumer clears the flag, so a completed launch leaves
 // the flag array zero for the next one (the caller zero-fills the workspace
-// once).  A wait that polls more than the thread's spin limit
+// once).  Round 4: the producer raises its flag once the state stores are
+// acknowledged but after its y stores are issued (a counted vmcnt), and
+// k_chain_tile's consumer polls once before its x window loads: if the flag
+// is already up (the common case: the producer ran a dispatch generation
+// earlier), the state comes by an sc1 LDS-DMA issued after that poll, behind
+// the SRC and pass 1 (chain_tile_body); else it waits as described.  A wait that polls more than the thread's spin limit
 // (dsp_chain_spin_limit; default 2^23 polls with s_sleep 2 between them,
 // ~0.4 s: a broken dispatch order, or a GPU time-sliced between processes)
 // gives up: it sets the workspace's status word (dsp_chain_status reports it,
