@@ -559,6 +559,12 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
   // Opaque uniform bounds: otherwise the compiler clips to +-1 and selects the
   // unclipped value per sample (4 VALU per sample instead of max + min).
   asm volatile("" : "+v"(lo), "+v"(hi));
+  // The realisation's input gain prod(b0) moves to the output, after the
+  // float32 conversion: the recursion runs on y with every state scaled by
+  // 1 / gain (the tables' Q carries the 1 / gain, so the carry and the entry
+  // states are in those coordinates), and z = fl32(v) * gain32 -- one float32
+  // multiply per sample instead of a float64 one (two roundings: <= 1.5 ulp).
+  const float g32 = (float)mt->gain;
   {
     double pend[kS];  // pend[k]: stage k's output from the previous step
 #pragma unroll
@@ -567,14 +573,15 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
       for (int k = kS - 1; k >= 0; --k) {
         const int t = st - k;
         if (t < 0 || t >= TS) continue;
-        const double u = k == 0 ? (double)y[t] * mt->gain : pend[k - 1];
+        const double u = k == 0 ? (double)y[t] : pend[k - 1];
         const double c1 = mt->cf[k][0], c2 = mt->cf[k][1], a1 = mt->cf[k][2], a2 = mt->cf[k][3];
         const double w = fma(-a2, s2[k], fma(-a1, s1[k], u));
         const double v2 = fma(c2, s2[k], fma(c1, s1[k], w));
         s2[k] = s1[k];
         s1[k] = w;
         if (k == kS - 1)
-          y[t] = NANCLIP ? clip_f32((float)v2, lo, hi) : __builtin_amdgcn_fmed3f((float)v2, lo, hi);
+          y[t] = NANCLIP ? clip_f32((float)v2 * g32, lo, hi)
+                         : __builtin_amdgcn_fmed3f((float)v2 * g32, lo, hi);
         else pend[k] = v2;
       }
     }
@@ -1543,7 +1550,7 @@ uint64_t tables_key(const TilePlan& tp, int64_t n_in, int64_t n_out, int K, int 
       h *= 1099511628211ull;
     }
   };
-  const int64_t v[] = {3 /* table layout version */, tp.kind, tp.tsub, n_in, n_out, K, L, M, c, S,
+  const int64_t v[] = {4 /* table layout version */, tp.kind, tp.tsub, n_in, n_out, K, L, M, c, S,
                        (int64_t)sizeof(TileTables)};
   mix(v, sizeof(v));
   if (S > 0 && sos) mix(sos, sizeof(double) * 5 * (size_t)S);
@@ -1928,6 +1935,9 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
     tt->cf[k][3] = p.c[k][4];
   }
   tt->gain = p.G;
+  // pass 2 applies the gain at the output (pass2_cascade): states in 1 / gain
+  for (int r = 0; r < kD; ++r)
+    for (int c = 0; c < kD; ++c) tt->Q[r][c] /= p.G;
   tt->tsub = (int32_t)tp.tsub;
   tt->np = tp.kind == 1 ? Geo3241::NP : 0;
   tt->L = L;

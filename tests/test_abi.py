@@ -263,8 +263,10 @@ def test_chain_tile_tables_host_only():
     block-diagonal carry tables reproduce the cascade's dense state algebra
     (T D^(48 2^d) T^-1 = A^(48 2^d); T sum_i G'[i] y[i] = the zero-state end
     state of a 48-sample sub-chunk); the float32 pass-1 rows in input-normal
-    coordinates give the same end state through Q (T Q sum_i Gc[i] y[i]), Q is
-    lower triangular and the coordinates have unit variance under white noise;
+    coordinates give the same end state through Q (gain T Q sum_i Gc[i] y[i]:
+    pass 2 applies the realisation's gain at the output, so its states and Q
+    carry 1 / gain), Q is lower triangular and the coordinates have unit
+    variance under white noise;
     the tap pairs are the reversed polyphase branches shifted by their window
     parity; the key fingerprints geometry and cascade; config 5's geometry
     builds 32-sample tables for the generic kernel; others decline with 1."""
@@ -312,8 +314,10 @@ def test_chain_tile_tables_host_only():
     Q = tb["Q"]
     Gc = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)   # rows 2j, 2j+1
     assert np.array_equal(Q, np.tril(Q)) and not Gc[48:].any()
-    np.testing.assert_allclose(T @ (Q @ (Gc[:48].T @ y)), X, rtol=1e-5, atol=1e-6 * np.abs(X).max())
-    P = T @ Q                                   # DF2 coordinates = P * input-normal ones
+    g0 = float(tb["gain"])
+    np.testing.assert_allclose(g0 * (T @ (Q @ (Gc[:48].T @ y))), X, rtol=1e-5,
+                               atol=1e-6 * np.abs(X).max())
+    P = g0 * (T @ Q)                            # DF2 coordinates = P * input-normal ones
     W = np.zeros((12, 12))                      # state covariance, unit white noise
     g = B.copy()
     for _ in range(60000):
@@ -355,7 +359,7 @@ def test_chain_tile_tables_host_only():
         X = A5 @ X + B5 * float(v)
     np.testing.assert_allclose(tb["T"] @ (tb["G"][:32].T @ y), X, rtol=1e-10, atol=1e-12)
     Gc5 = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)
-    np.testing.assert_allclose(tb["T"] @ (tb["Q"] @ (Gc5[:32].T @ y)), X,
+    np.testing.assert_allclose(float(tb["gain"]) * (tb["T"] @ (tb["Q"] @ (Gc5[:32].T @ y))), X,
                                rtol=1e-5, atol=1e-6 * np.abs(X).max())
     assert not tb["TP"].any()
     # class tables: sub-chunks start at outputs 32 j; class j mod 5 (32*147 mod 160 = 64)
