@@ -1312,22 +1312,60 @@ __device__ __forceinline__ void gct_tile(const TileArgs& a, const float* seq, fl
     f32x2 X[NPW];
 #pragma unroll
     for (int m = 0; m < NPW; ++m) X[m] = f32x2{xl[2 * m], xl[2 * m + 1]};
+    // Outputs in pairs, the next pair's tap rows read while this one computes
+    // and the two FMA chains interleaved (each output's own chain, pairs in
+    // ascending order, is unchanged: y bitwise the same).  Against one output
+    // at a time: 1.128 -> 1.122 ms at config 5 (profiles/r04_gct_pairs_ab.txt);
+    // groups of 4 spill.
+    constexpr int G = 2;
+    static_assert(kGenTS % G == 0, "whole groups");
+    struct Row {
+      f32x4 t0, t1;
+      f32x2 t2;
+    };
+    auto load_row = [&](int i) {
+      Row r;
+      r.t0 = *reinterpret_cast<const f32x4*>(row + kCtRow * i);
+      r.t1 = *reinterpret_cast<const f32x4*>(row + kCtRow * i + 4);
+      if (!(T7 && ((i * M / L) % 2 == 0)))
+        r.t2 = *reinterpret_cast<const f32x2*>(row + kCtRow * i + 8);
+      else
+        r.t2 = f32x2{0.f, 0.f};
+      return r;
+    };
+    Row cur[G];
 #pragma unroll
-    for (int i = 0; i < kGenTS; ++i) {
-      const int g2 = (i * M / L) / 2;
-      const bool last = !(T7 && ((i * M / L) % 2 == 0));
-      const f32x4 t0 = *reinterpret_cast<const f32x4*>(row + kCtRow * i);
-      const f32x4 t1 = *reinterpret_cast<const f32x4*>(row + kCtRow * i + 4);
-      f32x2 acc = {0.f, 0.f};
-      acc = __builtin_elementwise_fma(f32x2{t0.x, t0.y}, X[g2], acc);
-      acc = __builtin_elementwise_fma(f32x2{t0.z, t0.w}, X[g2 + 1], acc);
-      acc = __builtin_elementwise_fma(f32x2{t1.x, t1.y}, X[g2 + 2], acc);
-      acc = __builtin_elementwise_fma(f32x2{t1.z, t1.w}, X[g2 + 3], acc);
-      if (last) {
-        const f32x2 t2 = *reinterpret_cast<const f32x2*>(row + kCtRow * i + 8);
-        acc = __builtin_elementwise_fma(t2, X[g2 + 4], acc);
+    for (int o = 0; o < G; ++o) cur[o] = load_row(o);
+#pragma unroll
+    for (int i0 = 0; i0 < kGenTS; i0 += G) {
+      Row nxt[G];
+      if (i0 + G < kGenTS) {
+#pragma unroll
+        for (int o = 0; o < G; ++o) nxt[o] = load_row(i0 + G + o);
       }
-      y[i] = acc.x + acc.y;
+      f32x2 acc[G];
+#pragma unroll
+      for (int o = 0; o < G; ++o) acc[o] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int pp = 0; pp < 5; ++pp) {
+#pragma unroll
+        for (int o = 0; o < G; ++o) {
+          const int i = i0 + o;
+          const int g2 = (i * M / L) / 2;
+          const bool last = !(T7 && ((i * M / L) % 2 == 0));
+          if (pp == 4 && !last) continue;
+          const f32x2 t = pp == 0   ? f32x2{cur[o].t0.x, cur[o].t0.y}
+                          : pp == 1 ? f32x2{cur[o].t0.z, cur[o].t0.w}
+                          : pp == 2 ? f32x2{cur[o].t1.x, cur[o].t1.y}
+                          : pp == 3 ? f32x2{cur[o].t1.z, cur[o].t1.w}
+                                    : cur[o].t2;
+          acc[o] = __builtin_elementwise_fma(t, X[g2 + pp], acc[o]);
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < G; ++o) y[i0 + o] = acc[o].x + acc[o].y;
+#pragma unroll
+      for (int o = 0; o < G; ++o) cur[o] = nxt[o];
     }
   }
   pin(y);
