@@ -243,14 +243,14 @@ def kernel_bytes(chain, name):
 
 def valu_work(chain, mean_ms):
     """float64 FMA work of the single-pass kernel: per output
-    sample 24 (pass 2), plus per TS-sample sub-chunk the carry's 246 (Q e 78,
-    s = T m 60, the blocked scan 28 + 12 + 12 + 32, the entry state 24; static
-    ISA count of k_chain_tile: 1382 per 48-sample lane).  Pass 1 and the SRC
-    are float32 (v_pk_fma_f32).  None for the two-launch chain."""
+    sample 24 (pass 2), plus per TS-sample sub-chunk the carry's 210 (the change
+    of basis Q e, s = T m and the blocked scan: PMC SQ_INSTS_VALU_FMA_F64 per
+    wave is 1362 at TS = 48 and 978 at TS = 32, profiles/r04_m3_*).  Pass 1 and
+    the SRC are float32 (v_pk_fma_f32).  None for the two-launch chain."""
     ts = chain.tile_len
     if not ts:
         return None
-    per_sample = 24 + 246 / ts
+    per_sample = 24 + 210 / ts
     fma = per_sample * chain.B * chain.n_out
     tflops = 2 * fma / (mean_ms * 1e-3) / 1e12
     return {"bound": "package power (1400 W cap): fp64 + packed fp32 VALU on top of the HBM stream",
@@ -259,10 +259,11 @@ def valu_work(chain, mean_ms):
             "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
             "note": "beside the fp64 FMAs the kernel issues 19.7 (L3/M2: SRC 656 + pass 1 288 "
                     "per 48-sample lane sub-chunk) or 10 (generic) v_pk_fma_f32 per sample; it "
-                    "runs at the 1400 W package power cap and is VALU-issue-bound at the clock "
-                    "that leaves (config 4: 91 % of the kernel's cycles issue VALU at ~1.64 GHz, "
-                    "PMC, profiles/r04_m1_c4_pmc_summary.txt; a pure 1R:2W HBM stream at 5.1 TB/s "
-                    "draws ~865 W), DESIGN.md §3.0.2, §3.0.5"}
+                    "runs at the 1400 W package power cap, VALU-issue-bound at the clock that "
+                    "leaves (config 4: 89 % of the kernel's cycles issue VALU, PMC, "
+                    "profiles/r04_m3_c4_pmc_summary.txt; a pure 1R:2W HBM stream at 5.1 TB/s "
+                    "draws ~865 W), and moves ~0.8 of what such a stream reaches "
+                    "(mix_ceiling_gbs), DESIGN.md §3.0.2, §3.0.5"}
 
 
 def load_traffic(wl_name, channels):
