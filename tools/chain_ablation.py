@@ -28,34 +28,35 @@ ALL = ["BASE", "NOSRC", "NOP1", "NOSCAN", "NOP2", "NOYST", "NOZST"]
 def patched() -> str:
     s = open(os.path.join(CSRC, "chain_tile.hip")).read()
 
-    def rep(old, new):
+    def rep(old, new, count=1):
         nonlocal s
-        if old not in s:
+        if s.count(old) != count:
             raise SystemExit(f"chain_tile.hip changed; update the ablation patch near: {old[:60]!r}")
-        s = s.replace(old, new, 1)
+        s = s.replace(old, new)
 
-    parts = "".join(f"    src_part<GEO, {h}, 12>(xw, mt, y);\n    pin(y);\n" for h in (0, 12, 24, 36))
-    rep(parts, "#ifdef V_NOSRC\n#pragma unroll\n    for (int i = 0; i < TS; ++i) y[i] = xw[i];\n"
-        "    pin(y);\n#else\n" + parts + "#endif\n")
-    # pass 1 (float32 sums in input-normal coordinates, round 3): keep the
-    # change of basis, drop the 6 v_pk_fma_f32 per sample
+    # SRC: y = window samples (k_chain_tile's DLY part of 48 and plain parts of 24)
+    rep("    if constexpr (DLY) {\n      src_part<GEO, 0, 48, true>(xw, mt, y);",
+        "#ifdef V_NOSRC\n#pragma unroll\n    for (int i = 0; i < TS; ++i) y[i] = xw[i];\n"
+        "    if (false) {\n#else\n    if constexpr (DLY) {\n#endif\n      src_part<GEO, 0, 48, true>(xw, mt, y);")
+    # pass 1 (float32 sums in input-normal coordinates): keep the change of
+    # basis, drop the 6 v_pk_fma_f32 per sample
     rep("#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {",
         "#ifdef V_NOP1\n#pragma unroll\n    for (int d = 0; d < kD; ++d) e2[d] = f32x2{y[d], y[d + 1]};\n"
         "    if (false)\n#endif\n#pragma unroll\n    for (int j = 0; j < TS / 2; ++j) {")
-    # carry (round-3 blocked scan): keep the LDS rows, drop the recurrences and
-    # the segment Kogge-Stone (rows get E' as is)
+    # carry (blocked scan): keep the LDS rows, drop the recurrences and the
+    # segment Kogge-Stone (rows get E' as is)
     rep("  double u0 = e[0].x, u1 = e[0].y;\n", "  double u0 = e[0].x, u1 = e[0].y;\n#ifndef V_NOSCAN\n")
-    rep("  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)\n",
-        "#else\n  if (worker)\n    for (int i = 0; i < 8; ++i)\n"
-        "      *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * kb) = e[i];\n#endif\n"
-        "  // ---- 4. publish the tile's end state (segment 7's workers hold v_63)\n")
-    rep("    store_tile<TS>(lds, y, lane, ry, m0);\n",
-        "#ifndef V_NOYST\n    store_tile<TS>(lds, y, lane, ry, m0);\n#endif\n")
+    rep("  // ---- 4. publish the tile's end state",
+        "#else\n  for (int i = 0; i < 8; ++i)\n"
+        "    *reinterpret_cast<f64x2*>(rows + (8 * sg + i + 1) * kScanRow + 2 * (kb < 6 ? kb : 6)) = e[i];\n"
+        "#endif\n  // ---- 4. publish the tile's end state")
+    rep("    store_tile<TS>(lds, y, lane, ry);\n",
+        "#ifndef V_NOYST\n    store_tile<TS>(lds, y, lane, ry);\n#endif\n")
     rep("  {\n    double pend[kS];",
-        "#ifdef V_NOP2\n  for (int t = 0; t < TS; ++t) y[t] = clip_f32(y[t] + (float)s1[t % kS], lo, hi);\n"
+        "#ifdef V_NOP2\n  for (int t = 0; t < TS; ++t) y[t] = clip_f32(y[t] * g32 + (float)s1[t % kS], lo, hi);\n"
         "  if (false)\n#endif\n  {\n    double pend[kS];")
-    rep("  store_tile<TS>(lds, y, lane_z, rz, m0);",
-        "#ifndef V_NOZST\n  store_tile<TS>(lds, y, lane_z, rz, m0);\n#else\n"
+    rep("  store_tile<TS>(lds, y, lane_z, rz);",
+        "#ifndef V_NOZST\n  store_tile<TS>(lds, y, lane_z, rz);\n#else\n"
         "  if (y[0] == 12345.f) a.z[0] = y[1];\n#endif")
     return s
 
