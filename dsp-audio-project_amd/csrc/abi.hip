@@ -76,7 +76,10 @@ int dsp_version(void) {
   // propagate as through the reference's float64 convolution (round 4).
   // 2.2.0: dsp_pcm_batch_to_mono_f32 / dsp_pcm_batch_workspace_bytes (round 4).
   // 2.3.0: dsp_chain_path 2 / 3 pick the single-pass kernel variant (round 4).
-  return 20300;
+  // 2.4.0: inf / NaN through the FFT and spectrum entry points get the
+  // reference's labels (fft_nf.hip); dsp_fft_workspace_bytes adds the
+  // four-step's per-row header (round 5).
+  return 20400;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
@@ -258,8 +261,10 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                               state_table, scratch_bytes ? scratch : nullptr, scratch_bytes, s);
   }
   if (rc) return rc;
+  // after the clip z holds no inf, and NaN alone gives every bin NaN as in the
+  // reference: the non-finite repair runs only when the cascade does not clip
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,
-                              twiddles, nullptr, 0, s);
+                              twiddles, nullptr, 0, s, clip == 0);
 }
 
 int dsp_wav_parse(const uint8_t* file, size_t len, dsp_wav_info* info) {

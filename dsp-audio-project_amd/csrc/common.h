@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cmath>
 #include <cstdint>
@@ -222,10 +223,14 @@ int launch_biquad(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
 int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,
-                    void* ws, size_t ws_bytes, hipStream_t s);
+                    void* ws, size_t ws_bytes, hipStream_t s, bool repair = true);
+// repair: run the non-finite repair (fft_nf.hip) after the transform; a caller
+// whose input holds no inf (the chain after its clip: NaN alone already gives
+// the reference's all-NaN spectrum) may skip it.  Above DSP_MAX_LOG2N the
+// repair always runs.
 int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
                 int64_t seg_len, int64_t hop, int64_t frames, int log2n, int64_t ld_mag,
-                const float* window, const float* tw, hipStream_t s);
+                const float* window, const float* tw, hipStream_t s, bool repair = true);
 int bluestein_log2m(int64_t n);
 int launch_dft(const float* in, float* out, int64_t B, int64_t n, int real_in, int64_t ld_in,
                int64_t ld_out, const float* chirp, const float* chirp_fft, const float* tw_m,
@@ -234,6 +239,27 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, void* ws, size_t ws_bytes,
                hipStream_t s);
 size_t fft_workspace_bytes(int64_t B, int log2n);
+
+// Non-finite input through the power-of-two FFT / spectrum (fft_nf.hip): the
+// reference's inf / NaN labels restored after the fast transform.  mode: 0
+// complex rows in, 1 real rows in (both complex out), 2 windowed magnitude
+// spectrum (segment / frame framing as dsp_stft_mag_f32).
+struct NfArgs {
+  const float* in;
+  float* out;
+  int64_t B, ld_in, ld_out;
+  int64_t seg_start, seg_len, hop, frames;
+  const float* win;
+  const float* tw;
+  int mode, log2n;
+};
+// log2n <= DSP_MAX_LOG2N: after any fast kernel (no workspace).
+int launch_nf_small(const NfArgs& a, hipStream_t s);
+// log2n > DSP_MAX_LOG2N, B <= 65535 rows: hdr (2 words per row: flag set by the
+// four-step's first step, list length, both zeroed before it), lists (row r's
+// at lists + r * list_stride words, >= N words each).
+int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint32_t* lists, int64_t list_stride,
+                    hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 
 // Audio I/O (audio_io.hip).

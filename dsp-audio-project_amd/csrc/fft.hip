@@ -952,7 +952,33 @@ struct Fft4Args {
   FftArgs a;          // in / out / rows / segment / window / W_N table
   float2* ws;         // B x N complex
   int64_t N;          // NA * NB
+  uint32_t* hdr;      // per row: non-finite flag, list length (fft_nf.hip)
 };
+
+// Step A's input: a non-finite value sets `nf` (the row's flag for the
+// non-finite repair, fft_nf.hip) and, for the complex transforms, reads as
+// zero, so that the output holds the DFT of the finite part -- the values the
+// reference gives the components that no inf or NaN reaches.  (The spectrum's
+// bins all become +inf or NaN; the repair rewrites every one.)
+template <int MODE>
+__device__ __forceinline__ float2 load_input_nf(const FftArgs& a, const InRow& r, int n, bool& nf) {
+  if constexpr (MODE == kSpec) {
+    const float s = (n < r.valid) ? a.in[r.base + n] : 0.f;
+    nf |= !__builtin_isfinite(s);
+    return make_float2(s * a.win[n], 0.f);
+  } else {
+    float2 v = load_input<MODE>(a, r, n, true);
+    if (!__builtin_isfinite(v.x)) {
+      nf = true;
+      v.x = 0.f;
+    }
+    if (!__builtin_isfinite(v.y)) {
+      nf = true;
+      v.y = 0.f;
+    }
+    return v;
+  }
+}
 
 template <int LOG2A, int MODE>
 __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
@@ -965,10 +991,12 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
   const int64_t b = blockIdx.y;
   const int64_t c0 = (int64_t)blockIdx.x * KC;
   const InRow ir = in_row<MODE>(a, b);
+  bool nf = false;
   for (int i = threadIdx.x; i < KC * NA; i += NT) {
     const int c = i % KC, n2 = i / KC;
-    lds[c * TS + lpad(n2)] = load_input<MODE>(a, ir, (int)(c0 + c + NB * n2), true);
+    lds[c * TS + lpad(n2)] = load_input_nf<MODE>(a, ir, (int)(c0 + c + NB * n2), nf);
   }
+  if (nf) f.hdr[2 * b] = 1u;
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2A, 0> tw;
   load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA);
@@ -1203,13 +1231,19 @@ int dispatch(const FftArgs& a, int log2n, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
+}  // namespace
+
+// [Y: B x N complex][non-finite header: 2 words per row of a launch part]
 size_t fft_workspace_bytes(int64_t B, int log2n) {
   if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
-  return mul_sat((size_t)B, (size_t)1 << log2n, sizeof(float2));
+  const size_t rows = (size_t)(B < kMaxRows4 ? B : kMaxRows4);
+  return add_sat(mul_sat((size_t)B, (size_t)1 << log2n, sizeof(float2)),
+                 mul_sat(rows, 2, sizeof(uint32_t)));
 }
 
 namespace {
-constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
 
 // Four-step transform of B rows, in launches of <= kMaxRows4 rows.
 template <int MODE>
@@ -1219,13 +1253,21 @@ int run_fft4(FftArgs a, int log2n, void* ws, size_t ws_bytes, hipStream_t s) {
   DSP_REQUIRE(ws && ws_bytes >= need, "FFT workspace too small: %zu < %zu bytes", ws_bytes, need);
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 7) == 0, "FFT workspace not 8-byte aligned");
   const int64_t B = a.B;
+  const int64_t N = int64_t(1) << log2n;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + (size_t)B * N * 8);
   for (int64_t b0 = 0; b0 < B; b0 += kMaxRows4) {
     FftArgs part = a;
     part.B = B - b0 < kMaxRows4 ? B - b0 : kMaxRows4;
     part.in = a.in + b0 * a.ld_in * (MODE == kC2C ? 2 : 1);
     part.out = a.out + b0 * a.ld_out * (MODE == kSpec ? 1 : 2);
-    const Fft4Args f{part, static_cast<float2*>(ws), int64_t(1) << log2n};
+    DSP_HIP(hipMemsetAsync(hdr, 0, (size_t)part.B * 2 * sizeof(uint32_t), s));
+    const Fft4Args f{part, static_cast<float2*>(ws), N, hdr};
     if (int rc = dispatch4<MODE>(f, log2n, s)) return rc;
+    // the rows' non-finite inputs, listed in the freed Y rows
+    const NfArgs nfa{part.in, part.out, part.B, part.ld_in, part.ld_out, part.seg_start,
+                     part.seg_len, part.hop, part.frames, part.win,
+                     reinterpret_cast<const float*>(part.tw), MODE, log2n};
+    if (int rc = launch_nf_large(nfa, hdr, static_cast<uint32_t*>(ws), 2 * N, s)) return rc;
   }
   return DSP_OK;
 }
@@ -1234,7 +1276,7 @@ int run_fft4(FftArgs a, int log2n, void* ws, size_t ws_bytes, hipStream_t s) {
 int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t seg_start, int64_t seg_len, int log2n,
                     int64_t ld_mag, const float* window, const float* tw,
-                    void* ws, size_t ws_bytes, hipStream_t s) {
+                    void* ws, size_t ws_bytes, hipStream_t s, bool repair) {
   if (log2n > DSP_MAX_LOG2N) {
     DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n,
                 DSP_MAX_LOG2N_FFT);
@@ -1251,12 +1293,13 @@ int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
     TraceScope trace("spectrum", s);
     return run_fft4<kSpec>(a, log2n, ws, ws_bytes, s);
   }
-  return launch_stft(x, mag, B, ld_x, seg_start, seg_len, 0, 1, log2n, ld_mag, window, tw, s);
+  return launch_stft(x, mag, B, ld_x, seg_start, seg_len, 0, 1, log2n, ld_mag, window, tw, s,
+                     repair);
 }
 
 int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg_start,
                 int64_t seg_len, int64_t hop, int64_t frames, int log2n, int64_t ld_mag,
-                const float* window, const float* tw, hipStream_t s) {
+                const float* window, const float* tw, hipStream_t s, bool repair) {
   DSP_REQUIRE(log2n >= 0 && log2n <= DSP_MAX_LOG2N, "log2n=%d outside [0, %d]", log2n,
               DSP_MAX_LOG2N);
   const int64_t N = int64_t(1) << log2n;
@@ -1272,8 +1315,15 @@ int launch_stft(const float* x, float* mag, int64_t B, int64_t ld_x, int64_t seg
   DSP_REQUIRE(B <= INT64_MAX / frames, "too many frames");
   FftArgs a{x, mag, B * frames, ld_x, ld_mag, seg_start, seg_len, hop, frames, window,
             reinterpret_cast<const float2*>(tw)};
-  TraceScope trace(frames == 1 ? "spectrum" : "stft", s);
-  return dispatch_spec(a, log2n, s);
+  {
+    TraceScope trace(frames == 1 ? "spectrum" : "stft", s);
+    if (int rc = dispatch_spec(a, log2n, s)) return rc;
+  }
+  if (!repair) return DSP_OK;
+  TraceScope trace("spectrum_nf", s);
+  return launch_nf_small(NfArgs{x, mag, B * frames, ld_x, ld_mag, seg_start, seg_len, hop, frames,
+                                window, tw, kSpec, log2n},
+                         s);
 }
 
 int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
@@ -1289,11 +1339,19 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                   (real_in || (reinterpret_cast<uintptr_t>(in) & 7) == 0),
               "complex buffers must be 8-byte aligned");
   FftArgs a{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, reinterpret_cast<const float2*>(tw)};
-  TraceScope trace("fft", s);
-  if (log2n > DSP_MAX_LOG2N)
+  if (log2n > DSP_MAX_LOG2N) {
+    TraceScope trace("fft", s);
     return real_in ? run_fft4<kR2C>(a, log2n, ws, ws_bytes, s)
                    : run_fft4<kC2C>(a, log2n, ws, ws_bytes, s);
-  return real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s);
+  }
+  {
+    TraceScope trace("fft", s);
+    if (int rc = real_in ? dispatch<kR2C>(a, log2n, s) : dispatch<kC2C>(a, log2n, s)) return rc;
+  }
+  TraceScope trace("fft_nf", s);
+  return launch_nf_small(NfArgs{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, tw,
+                                real_in ? kR2C : kC2C, log2n},
+                         s);
 }
 
 }  // namespace dsp

@@ -108,7 +108,18 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
  * Up to DSP_MAX_LOG2N one launch keeps each transform in LDS and needs no
  * workspace; above it a four-step transform (two launches) keeps its
  * intermediate in `workspace` (device, 8-byte aligned,
- * >= dsp_fft_workspace_bytes(B, log2n) = B * N * 8 bytes; 0 below).
+ * >= dsp_fft_workspace_bytes(B, log2n) = B * N * 8 bytes plus a header of 8
+ * bytes per row (at most 65535 rows); 0 below).
+ * Non-finite input (ABI 2.4): every output component gets the class --
+ * finite, +inf, -inf or NaN -- that the reference's recursive radix-2 DIT in
+ * complex128 numpy arithmetic gives it (inf * 0 = NaN at the k = 0 twiddles,
+ * inf - inf = NaN), and a finite component the DFT of the input with its
+ * non-finite components zeroed (the reference's value there).  A repair
+ * launch after the transform does it; on finite data it exits at once (up to
+ * 2^14: one launch reading X[0] of every transform; above: the header flags).
+ * The same holds for dsp_spectrum_f32 and dsp_stft_mag_f32, whose |X| is +inf
+ * wherever a component is infinite and NaN where one is NaN, as np.abs
+ * (hypot) gives it (dsp_core.py:91).
  * ------------------------------------------------------------------------- */
 size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n);
 int dsp_fft_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20300     # 2.3.0: chain kernel variants (2.2.0: the batched loader)
+    assert lib.dsp_version() == 20400     # 2.4.0: FFT/spectrum non-finite repair (2.3.0: chain variants)
     assert isinstance(_lib.last_error(), str)
 
 
@@ -28,13 +28,15 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     assert rc == _lib.DSP_EINVAL and "L=0" in _lib.last_error()
     rc = lib.dsp_fft_c2c_f32(None, None, 1, 29, 1, 1 << 29, 1 << 29, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL
-    # four-step sizes need a workspace of B * N complex
+    # four-step sizes need a workspace of B * N complex plus the non-finite
+    # header, 8 bytes per row of a launch part (<= 65535 rows)
     assert lib.dsp_fft_workspace_bytes(3, 14) == 0
-    assert lib.dsp_fft_workspace_bytes(3, 15) == 3 * (1 << 15) * 8
-    assert lib.dsp_fft_workspace_bytes(3, 26) == 3 * (1 << 26) * 8
-    assert lib.dsp_fft_workspace_bytes(1, 28) == (1 << 28) * 8
+    assert lib.dsp_fft_workspace_bytes(3, 15) == 3 * (1 << 15) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 26) == 3 * (1 << 26) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(1, 28) == (1 << 28) * 8 + 8
     assert lib.dsp_fft_workspace_bytes(1, 29) == 0
-    assert lib.dsp_fft_workspace_bytes(3, 27) == 3 * (1 << 27) * 8
+    assert lib.dsp_fft_workspace_bytes(3, 27) == 3 * (1 << 27) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(70000, 15) == 70000 * (1 << 15) * 8 + 65535 * 8
     rc = lib.dsp_fft_c2c_f32(1024, 1024, 1, 15, 1, 1 << 15, 1 << 15, 1024, None, 0, None)
     assert rc == _lib.DSP_EINVAL and "workspace" in _lib.last_error()
     sos = (ctypes.c_double * 5)(1, 0, 0, 0, 0)
