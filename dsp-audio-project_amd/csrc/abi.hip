@@ -78,7 +78,7 @@ int dsp_version(void) {
   // 2.3.0: dsp_chain_path 2 / 3 pick the single-pass kernel variant (round 4).
   // 2.4.0: inf / NaN through the FFT and spectrum entry points get the
   // reference's labels (fft_nf.hip); dsp_fft_workspace_bytes adds the
-  // four-step's per-row header (round 5).
+  // four-step's per-row header; dsp_lfilter_nonfinite_f32 (round 5).
   return 20400;
 }
 
@@ -107,6 +107,15 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
   return dsp::launch_biquad(x, y, B, n, ld_x, ld_y, sos_host, S, clip, chunk_len,
                             state_table, workspace, workspace_bytes,
                             static_cast<hipStream_t>(stream));
+}
+
+int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                              int64_t ld_y, const double* b, int32_t nb, const double* a,
+                              int32_t na, void* stream) {
+  dsp::clear_error();
+  if (x && x == y) return dsp::set_error(DSP_EINVAL, "x and y must not alias");
+  return dsp::launch_lfilter_nf(x, y, B, n, ld_x, ld_y, b, nb, a, na,
+                                static_cast<hipStream_t>(stream));
 }
 
 size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n) {

@@ -261,6 +261,9 @@ int launch_nf_small(const NfArgs& a, hipStream_t s);
 int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint32_t* lists, int64_t list_stride,
                     hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
+// lfilter's non-finite labels after the cascade (lfilter_nf.hip).
+int launch_lfilter_nf(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x, int64_t ld_y,
+                      const double* b, int nb, const double* a, int na, hipStream_t s);
 
 // Audio I/O (audio_io.hip).
 int wav_parse(const uint8_t* buf, size_t len, dsp_wav_info* info);

@@ -31,6 +31,7 @@ DSP_MAX_STAGES = 16
 DSP_MAX_LOG2N = 14
 DSP_MAX_LOG2N_FFT = 28
 DSP_MAX_DFT = 8192
+DSP_LFILTER_NF_MAX = 4096
 
 _c_i32, _c_i64, _c_u64, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
 _vp, _dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
@@ -46,6 +47,8 @@ _SIGNATURES = {
     "dsp_biquad_cascade_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _dp, _c_i32, _c_i32, _c_i64,
         _vp, _vp, _c_sz, _vp]),
+    "dsp_lfilter_nonfinite_f32": (ctypes.c_int, [
+        _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _dp, _c_i32, _dp, _c_i32, _vp]),
     "dsp_fft_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
     "dsp_fft_c2c_f32": (ctypes.c_int, [
         _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),

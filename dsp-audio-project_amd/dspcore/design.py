@@ -194,13 +194,16 @@ class LfilterPlan:
     """How aplicar_ecuacion_diferencias runs lfilter(b, a, x) of any order
     (reference dsp_core.py:205-214): 'sos' -- the transfer function as
     second-order sections (float64, host) for the biquad-cascade kernel;
-    'fir' -- a pure FIR (a == [1] after normalisation, more than 3 taps) as a
-    causal convolution on the SRC kernel with L = M = 1; 'gain' -- b and a of
-    length 1 (y = b0/a0 x)."""
+    'fir' -- a of length 1, where lfilter is the convolution np.convolve(b / a0,
+    x)[:n] (a gain when b has length 1), as a causal convolution on the SRC
+    kernel with L = M = 1.  That keeps lfilter's non-finite semantics of the
+    case: an inf or NaN meets every tap of b, a zero tap included (0 * inf =
+    NaN), and stays within len(b) samples."""
     kind: str
     sos: np.ndarray | None = None
     taps: np.ndarray | None = None
-    gain: float = 1.0
+    b: np.ndarray | None = None     # 'sos': lfilter's b / a0 and a / a0 (the
+    a: np.ndarray | None = None     # non-finite relabelling, dsp_lfilter_nonfinite_f32)
 
 
 MAX_LFILTER_SECTIONS = 16     # include/dspcore.h DSP_MAX_STAGES: sections per cascade launch
@@ -225,20 +228,17 @@ def lfilter_plan(b, a) -> LfilterPlan:
         raise ValueError("BUG: filter coefficient a[0] == 0 not supported yet")
     b = b / a[0]
     a = a / a[0]
+    if a.size == 1:      # scipy's lfilter convolves here (the DF2T recursion below)
+        return LfilterPlan("fir", taps=b.copy())
     a_tail = np.trim_zeros(a[1:], "b")
-    if a_tail.size == 0:
-        if b.size == 1:
-            return LfilterPlan("gain", gain=float(b[0]))
-        if b.size > 3:
-            return LfilterPlan("fir", taps=b.copy())
     if max(a.size, b.size) <= 3:
-        return LfilterPlan("sos", sos=tf_to_sos_row(b, a).reshape(1, 5))
+        return LfilterPlan("sos", sos=tf_to_sos_row(b, a).reshape(1, 5), b=b, a=a)
     import scipy.signal
-    a = np.concatenate([[1.0], a_tail])
-    sos6 = scipy.signal.tf2sos(b, a)            # rows b0 b1 b2 a0(=1) a1 a2
+    sos6 = scipy.signal.tf2sos(b, np.concatenate([[1.0], a_tail]))  # rows b0 b1 b2 1 a1 a2
     sos = np.ascontiguousarray(np.column_stack([sos6[:, 0:3] / sos6[:, 3:4],
                                                 sos6[:, 4:6] / sos6[:, 3:4]]))
-    return LfilterPlan("sos", sos=sos)
+    # (b and the untrimmed a: lfilter's recursion order counts a's trailing zeros)
+    return LfilterPlan("sos", sos=sos, b=b, a=a)
 
 
 def lfilter_groups(sos: np.ndarray) -> list[np.ndarray]:

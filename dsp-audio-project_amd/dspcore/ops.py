@@ -181,6 +181,27 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     return out
 
 
+def lfilter_nonfinite(x: torch.Tensor, y: torch.Tensor, b: np.ndarray, a: np.ndarray) -> torch.Tensor:
+    """Gives y = lfilter(b, a, x) (len(a) >= 2), computed by the cascade kernel,
+    scipy's inf / NaN labels from x's first non-finite sample on
+    (dsp_lfilter_nonfinite_f32); rows without one are left as they are."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    B, n = x.shape
+    if tuple(y.shape) != (B, n) or y.dtype != torch.float32 or y.stride(1) != 1:
+        raise ValueError("y must be float32 [B, n] with unit column stride")
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.dsp_lfilter_nonfinite_f32(_ptr(x), _ptr(y), B, n, ld(x), ld(y),
+                                           b.ctypes.data_as(_lib._dp), b.size,
+                                           a.ctypes.data_as(_lib._dp), a.size, _stream(x.device))
+    _lib.check(rc, "dsp_lfilter_nonfinite_f32")
+    return y
+
+
 def _dft_tables(n: int, device: torch.device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     def build():
         from .design import bluestein_tables

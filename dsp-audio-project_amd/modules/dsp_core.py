@@ -265,10 +265,13 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
 
     Biquads and second-order sections of higher IIR orders (design.lfilter_plan,
     float64 on the host) run on the float64 biquad-cascade kernel, 16 sections
-    a launch (float32 between launches, above order 32); a pure FIR
-    longer than 3 taps runs as a causal convolution on the SRC kernel (L = M =
-    1, float32 taps and sums); b/a of length 1 is a gain.  a[0] == 0 raises
-    ValueError as lfilter does.
+    a launch (float32 between launches, above order 32); with a of length 1,
+    where lfilter convolves, b runs as a causal convolution on the SRC kernel
+    (L = M = 1, float32 taps and sums; a gain is one tap), so an inf or NaN
+    stays within len(b) samples as in lfilter; otherwise, after the cascade,
+    one launch gives every output from the first inf or NaN on the +inf / -inf
+    / NaN that lfilter's recursion gives it (dsp_lfilter_nonfinite_f32; orders
+    up to 4096).  a[0] == 0 raises ValueError as lfilter does.
     """
     plan = _design.lfilter_plan(b, a)
     ops = _ops()
@@ -278,12 +281,11 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
             n = int(t.shape[1])
             src = _design.SrcPlan(1, 1, int(plan.taps.size), plan.taps, 0, n, n, 0)
             return ops.src_polyphase(t, src)
-        if plan.kind == "gain":
-            # one exact-product pass: the cascade kernel with the gain as b0
-            return _cascade(ops, t, np.array([[plan.gain, 0.0, 0.0, 0.0, 0.0]]), False, B)
+        x0 = t
         for group in _design.lfilter_groups(plan.sos):   # any order: <= 16 sections a launch
             t = _cascade(ops, t, group, False, B)
-        return t
+        # inf / NaN from x's first non-finite sample on as lfilter labels them
+        return ops.lfilter_nonfinite(x0, t, plan.b, plan.a)
     return _run(x_n, run, np.float64)
 
 

@@ -39,6 +39,7 @@ extern "C" {
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
 #define DSP_MAX_LOG2N_FFT 28 /* largest FFT / spectrum (four-step above 2^14)  */
 #define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
+#define DSP_LFILTER_NF_MAX 4096 /* largest order dsp_lfilter_nonfinite_f32 takes */
 
 /* ABI version (major*10000 + minor*100 + patch). */
 int dsp_version(void);
@@ -95,6 +96,26 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
                            int32_t S, int32_t clip, int64_t chunk_len,
                            const double* state_table, void* workspace,
                            size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * lfilter's inf / NaN labels after a cascade (ABI 2.4).
+ * Replaces nothing numeric: it relabels, after dsp_biquad_cascade_f32 (or
+ * consecutive calls of it) has filtered x into y with the second-order
+ * sections of lfilter(b, a) (dsp_core.py:214, len(a) >= 2), the outputs that
+ * a non-finite input reaches: scipy's recursion (direct form II transposed
+ * over b / a0 and a / a0 zero-padded to one length D + 1) gives every y from
+ * the first inf or NaN of x on the class -- +inf, -inf or NaN -- that its
+ * float64 arithmetic gives (a one-pole low-pass keeps +inf, a section with b1
+ * == a1 makes NaN), while the cascade makes them all NaN.  Rows whose y[n-1]
+ * is finite (no non-finite input) are left as they are, after one read.
+ * b (nb >= 1) and a (na >= 2, a[0] != 0) are HOST float64 arrays; D =
+ * max(na, nb) - 1 <= DSP_LFILTER_NF_MAX.  x and y are [B][ld] float32 device
+ * rows and must not alias.  (len(a) == 1 is lfilter's convolution: run it on
+ * dsp_src_polyphase_f32 with L = M = 1, c_offset = 0, which keeps its labels.)
+ * ------------------------------------------------------------------------- */
+int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, int64_t ld_x,
+                              int64_t ld_y, const double* b, int32_t nb, const double* a,
+                              int32_t na, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Batched complex FFT of power-of-two length, natural-order output: the DFT

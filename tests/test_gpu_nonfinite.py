@@ -402,3 +402,64 @@ def test_nonfinite_repair_leaves_finite_batches_alone(gpu):
     keep = np.arange(300) != 137
     np.testing.assert_array_equal(a[keep], b[keep])
     assert not np.isfinite(b[137]).any()
+
+
+# ---------------------------------------------------------------------------
+# aplicar_ecuacion_diferencias (dsp_core.py:205-214: scipy.signal.lfilter)
+# ---------------------------------------------------------------------------
+LFILTER_CASES = [
+    # len(a) == 1: lfilter's convolution (SRC kernel, L = M = 1)
+    ("gain", [3.0], [4.0]),
+    ("fir 2", [0.5, -0.5], [1.0]),
+    ("fir 3 with a zero tap", [1.0, 0.0, 2.0], [1.0]),
+    ("fir 31", list(np.hanning(31)), [2.0]),
+    # len(a) >= 2: the recursion (cascade kernel + dsp_lfilter_nonfinite_f32)
+    ("one-pole low-pass (inf persists)", [0.5, 0.5], [1.0, -0.3]),
+    ("one-pole, negative pole (inf alternates)", [1.0], [1.0, 0.6]),
+    ("peaking biquad (b1 == a1: NaN)", None, None),
+    ("fir through the recursion (a = [1, 0])", [1.0, 2.0, 3.0], [1.0, 0.0]),
+    ("trailing zeros of a count", [1.0], [1.0, -0.5, 0.0, 0.0]),
+    ("b longer than a", [0.2, 0.3, -0.1, 0.05, 0.4, 0.1], [1.0, -0.5, 0.2]),
+    ("butter 4 (four sections' worth of order)", "butter", None),
+]
+
+
+def _lfilter_coeffs(b, a):
+    import scipy.signal as ss
+    if b is None:
+        from dspcore import design
+        return design.peaking_biquad(1000.0, 48000.0, 6.0)
+    if b == "butter":
+        return ss.butter(4, 0.2)
+    return np.asarray(b, dtype=np.float64), np.asarray(a, dtype=np.float64)
+
+
+@pytest.mark.parametrize("name,b,a", LFILTER_CASES, ids=[c[0] for c in LFILTER_CASES])
+def test_nonfinite_lfilter_matches_scipy(gpu, name, b, a):
+    """aplicar_ecuacion_diferencias on rows with NaN / +inf / -inf at the
+    first and last samples, in the middle, two of opposite sign, one of each:
+    y's NaN / +inf / -inf masks are lfilter's exactly (a gain or FIR keeps an
+    inf within len(b) samples; a recursion labels everything after it, a
+    one-pole low-pass +inf forever, a peaking section NaN), finite samples
+    within 1e-5 (relative to max|y| above 1), 2-D batch and 1-D row."""
+    import scipy.signal as ss
+    from modules import dsp_core as dc
+    b, a = _lfilter_coeffs(b, a)
+    n = 3000
+    specs = [[(0, INF)], [(n - 1, NAN)], [(1500, -INF)], [(700, INF), (701, -INF)],
+             [(900, NAN), (2000, INF)], [(1200, INF), (1260, INF)], []]
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, (len(specs), n)).astype(np.float32)
+    for r, sp in enumerate(specs):
+        for pos, val in sp:
+            x[r, pos] = val
+    with _quiet():
+        want = [ss.lfilter(b, a, row.astype(np.float64)) for row in x]
+        y = dc.aplicar_ecuacion_diferencias(x, b, a)
+        y1 = dc.aplicar_ecuacion_diferencias(x[3], b, a)
+    assert y.dtype == np.float64 and y.shape == x.shape
+    for r in range(x.shape[0]):
+        fin = np.isfinite(want[r])
+        scale = max(1.0, float(np.max(np.abs(want[r][fin]))) if fin.any() else 1.0)
+        _same(y[r], want[r], EQ_ATOL * scale, f"{name} row {r} {specs[r]}")
+    _same(y1, want[3], EQ_ATOL * 10, f"{name} 1-D")

@@ -227,6 +227,10 @@ def _lfilter_cases():
         ("fir 31", ss.firwin(31, 0.2), [1.0]),
         ("fir 5, a = [2]", [1.0, 2.0, 3.0, 2.0, 1.0], [2.0]),
         ("gain", [3.0], [4.0]),
+        ("fir 3 with a zero tap", [1.0, 0.0, 2.0], [1.0]),
+        ("fir 2, a = [2]", [0.5, -0.5], [2.0]),
+        ("fir 5 through the recursion (a = [1, 0])", [1.0, 2.0, 3.0, 4.0, 5.0], [1.0, 0.0]),
+        ("gain through the recursion (a = [2, 0])", [3.0], [2.0, 0.0]),
     ]
 
 
@@ -245,10 +249,9 @@ def test_lfilter_plan_any_order_matches_lfilter():
             sos6 = np.column_stack([plan.sos[:, :3], np.ones(plan.sos.shape[0]), plan.sos[:, 3:]])
             got = ss.sosfilt(sos6, x)
             assert plan.sos.shape[0] <= design.MAX_LFILTER_SECTIONS
-        elif plan.kind == "fir":
-            got = np.convolve(x, plan.taps)[:x.size]
         else:
-            got = plan.gain * x
+            assert plan.kind == "fir" and np.size(a) == 1
+            got = np.convolve(x, plan.taps)[:x.size]
         assert np.max(np.abs(got - ref)) <= 1e-9 * max(1.0, np.max(np.abs(ref))), name
     with pytest.raises(ValueError, match="a\\[0\\] == 0"):
         design.lfilter_plan([1.0], [0.0, 1.0])
