@@ -127,18 +127,22 @@ def rank_channels(total: int, rank: int, world: int) -> tuple[int, int]:
 PREHEAT_S = 0.3   # untimed steps before the warmup: GPU clocks settle
 
 
-def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
+def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S, same_node=True,
+               stats=None):
     """Untimed steps for PREHEAT_S seconds (the MI355X boosts, then throttles,
     then settles over the first ~20-40 ms of a busy GPU: a 1 ms config-3 step
     measured 0.86 -> 1.19 -> 0.89 ms over its first 20 launches), then W untimed
     warmup steps, then K steps bracketed by barrier + sync on both sides.
     Returns the elapsed seconds; with `dist` initialised (a gloo group) the
-    job's time over all ranks, max(end) - min(start) on the host's monotonic
-    clock (perf_counter is CLOCK_MONOTONIC, one clock for every process of the
-    node): each rank stamps its start as it leaves the start barrier and its
-    end at its own final sync, so skew in leaving the barrier counts, and the
-    end barrier's gloo round trips (a sizeable share of a ~17 ms N = 8 timed
-    region) do not."""
+    job's time over all ranks.  When every rank runs on this node
+    (`same_node`, from the gathered host names) that is max(end) - min(start)
+    on the host's monotonic clock (perf_counter is CLOCK_MONOTONIC, one clock
+    for every process of the node): each rank stamps its start as it leaves
+    the start barrier and its end at its own final sync, so skew in leaving the
+    barrier counts, and the end barrier's gloo round trips (a sizeable share
+    of a ~17 ms N = 8 timed region) do not.  Across nodes the clocks are not
+    comparable, and it is the max over ranks of each rank's own elapsed time.
+    `stats` (a dict) receives this rank's own elapsed seconds as "local"."""
     t_pre = time.perf_counter()
     while preheat_s > 0:
         step()
@@ -156,14 +160,21 @@ def timed_loop(step, steps, warmup, sync, dist=None, preheat_s=PREHEAT_S):
         step()
     sync()
     elapsed = time.perf_counter() - t0
+    if stats is not None:
+        stats["local"] = elapsed
     if dist is not None:
         dist.barrier()
         import torch
-        t_end = torch.tensor([t0 + elapsed], dtype=torch.float64)
-        t_start = torch.tensor([t0], dtype=torch.float64)
-        dist.all_reduce(t_end, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t_start, op=dist.ReduceOp.MIN)
-        elapsed = float(t_end.item() - t_start.item())
+        if same_node:
+            t_end = torch.tensor([t0 + elapsed], dtype=torch.float64)
+            t_start = torch.tensor([t0], dtype=torch.float64)
+            dist.all_reduce(t_end, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t_start, op=dist.ReduceOp.MIN)
+            elapsed = float(t_end.item() - t_start.item())
+        else:
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
     return elapsed
 
 
@@ -253,7 +264,12 @@ def valu_work(chain, mean_ms):
     per_sample = 24 + 210 / ts
     fma = per_sample * chain.B * chain.n_out
     tflops = 2 * fma / (mean_ms * 1e-3) / 1e12
-    return {"bound": "package power (1400 W cap): fp64 + packed fp32 VALU on top of the HBM stream",
+    return {"kind": "model",
+            "model": "fp64 FMA per output sample = 24 (pass 2) + 210 / TS (carry), the static "
+                     "counts that SQ_INSTS_VALU_FMA_F64 / SQ_WAVES measured (1362 per wave at "
+                     "TS = 48, 978 at TS = 32, profiles/r04_m3_*); achieved = that work / this "
+                     "run's HIP-event mean, not a counter of this run",
+            "bound": "package power (1400 W cap): fp64 + packed fp32 VALU on top of the HBM stream",
             "fp64_fma_per_output_sample": round(per_sample, 3),
             "achieved": round(tflops, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
@@ -281,7 +297,7 @@ def load_traffic(wl_name, channels):
     return ent.get("per_launch", {}), ent.get("source")
 
 
-def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
+def measure(wl, B, steps, warmup, rank, world, dist, eager, device, same_node=True):
     """Builds the chain for B channels of workload wl, times K steps (graph
     replay unless eager) and a traced pass; returns the numbers."""
     import torch
@@ -317,7 +333,8 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
         except Exception as exc:  # noqa: BLE001  (fall back to eager launches)
             print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
     sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
-    elapsed = timed_loop(step, steps, warmup, sync, dist)
+    st = {}
+    elapsed = timed_loop(step, steps, warmup, sync, dist, same_node=same_node, stats=st)
     chain.check()      # raises HandoffError if a tile hand-off wait gave up
 
     # Traced pass: HIP events around every launch, on the kernels' stream.
@@ -333,8 +350,8 @@ def measure(wl, B, steps, warmup, rank, world, dist, eager, device):
         per.setdefault(name, []).append(ms)
     kernels = {k: round(sum(v) / len(v), 5) for k, v in per.items()}
     dom = max(kernels, key=kernels.get)
-    res = dict(chain=chain, elapsed=elapsed, launch=launch, kernels=kernels, dom=dom,
-               dom_bytes=kernel_bytes(chain, dom))
+    res = dict(chain=chain, elapsed=elapsed, local=st["local"], launch=launch, kernels=kernels,
+               dom=dom, dom_bytes=kernel_bytes(chain, dom))
     del x
     return res
 
@@ -351,7 +368,7 @@ def measure_stub(wl, B, steps):
     chain = SimpleNamespace(B=B, n_out=src.n_out, tile_len=0, cfg=SimpleNamespace(n_in=wl["n_in"]),
                             spec=spec, algorithmic_bytes=lambda: per * B)
     ms = 1e-6 * B + 1e-3
-    return dict(chain=chain, elapsed=steps * ms * 1e-3, launch="dry-run",
+    return dict(chain=chain, elapsed=steps * ms * 1e-3, local=steps * ms * 1e-3, launch="dry-run",
                 kernels={"chain_tile": ms}, dom="chain_tile", dom_bytes=kernel_bytes(chain, "chain_tile"))
 
 
@@ -526,6 +543,12 @@ def main(argv=None):
             os.dup2(saved, 1)
             os.close(saved)
         dist = tdist
+    same_node = True
+    if dist is not None:
+        import socket
+        hosts = [None] * world
+        dist.all_gather_object(hosts, socket.gethostname())
+        same_node = len(set(hosts)) == 1
     if dry:
         r = measure_stub(wl, B, args.steps)
         if dist is not None:
@@ -537,12 +560,34 @@ def main(argv=None):
         dev_index = int(os.environ.get("DSP_BENCH_DEVICE", local_rank))
         device = torch.device("cuda", dev_index)
         torch.cuda.set_device(device)
-        r = measure(wl, B, args.steps, args.warmup, rank, world, dist, args.eager, device)
+        r = measure(wl, B, args.steps, args.warmup, rank, world, dist, args.eager, device,
+                    same_node)
     chain, elapsed, kernels, dom = r["chain"], r["elapsed"], r["kernels"], r["dom"]
     if dist is not None and dry:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    per_rank = None
+    if dist is not None:
+        # every rank's own timed region, dominant-kernel mean and shard: the
+        # N > 1 line shows the spread (a slow or throttled GPU, an imbalance)
+        mine = torch.tensor([r["local"] * 1e3 / args.steps, kernels[dom], float(B)],
+                            dtype=torch.float64)
+        allr = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ms_r = [float(t[0]) for t in allr]
+        dom_r = [float(t[1]) for t in allr]
+        per_rank = {
+            "elapsed_ms_min": round(min(ms_r), 4), "elapsed_ms_max": round(max(ms_r), 4),
+            f"{dom}_ms_min": round(min(dom_r), 5), f"{dom}_ms_max": round(max(dom_r), 5),
+            "channels": [int(t[2]) for t in allr],
+            "elapsed_ms": [round(v, 4) for v in ms_r],
+            f"{dom}_ms": [round(v, 5) for v in dom_r],
+            "timing": ("max(end) - min(start), one node's monotonic clock" if same_node
+                       else "max over ranks of each rank's elapsed (ranks on several nodes)"),
+            "note": "elapsed_ms: per step, each rank's own timed region; "
+                    f"{dom}_ms: its HIP-event mean",
+        }
     ms_per_step = elapsed / args.steps * 1e3
     value = total * wl["n_in"] * args.steps / elapsed / 1e6
     mean_ms = kernels[dom]
@@ -617,6 +662,7 @@ def main(argv=None):
                 "algorithmic_bytes_per_gpu_step": chain_bytes,
             },
             "kernels_ms": kernels,
+            **({"per_rank": per_rank} if per_rank else {}),
             **{k: extras.get(k) for k in ("config3", "config4", "config5") if k in extras},
             "host_inclusive": extras.get("host_inclusive"),
             "copy_ceiling": extras.get("copy_ceiling"),

@@ -55,6 +55,31 @@ def test_two_rank_timing_is_max_over_ranks():
     assert (lo0, hi0, lo1, hi1) == (0, 16384, 16384, 32768)
 
 
+def _worker_nodes(rank, world, port, out):
+    """timed_loop with same_node=False: the max of the ranks' own times."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = {}
+        elapsed = bench.timed_loop(lambda: time.sleep(0.01 * (rank + 1)), steps=3, warmup=0,
+                                   sync=lambda: None, dist=dist, preheat_s=0, same_node=False,
+                                   stats=st)
+        out[rank] = (elapsed, st["local"])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_timed_loop_across_nodes_is_max_of_local_times():
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker_nodes, args=(world, _free_port(), out), nprocs=world, join=True)
+    (e0, l0), (e1, l1) = out[0], out[1]
+    assert e0 == e1 == pytest.approx(max(l0, l1))
+    assert l1 > l0
+
+
 def test_timed_loop_preheat_then_exact_counts():
     """bench.timed_loop runs untimed steps for preheat_s seconds, then exactly
     W warmup and K timed steps (the timed region covers only the K)."""
@@ -100,6 +125,13 @@ def test_bench_gpus_flag_launches_the_ranks_itself():
     assert out["config"]["channels_per_gpu"] == 16384
     assert out["config"]["parallelism"] == "channel-shard x2 (no collective)"
     assert out["cpu_baseline"] is None                  # N > 1: rank 0 skips the CPU leg
+    pr = out["per_rank"]                                # every rank's own numbers
+    assert pr["channels"] == [16384, 16384]
+    for k in ("elapsed_ms_min", "elapsed_ms_max", "chain_tile_ms_min", "chain_tile_ms_max"):
+        assert pr[k] > 0, k
+    assert pr["elapsed_ms_min"] <= pr["elapsed_ms_max"] and len(pr["elapsed_ms"]) == 2
+    assert pr["chain_tile_ms_min"] <= pr["chain_tile_ms_max"]
+    assert pr["timing"].startswith("max(end) - min(start)")   # both ranks on this host
 
 
 def test_bench_refuses_gpus_other_than_world_size():

@@ -19,6 +19,10 @@ def short(name):
     """Bench-trace name of a libdspcore kernel from its demangled symbol."""
     if "_repair" in name:
         return "chain_repair"
+    if "k_nf_small" in name or "k_nf_list" in name or "k_nf_fix" in name:
+        return "spectrum_nf"
+    if "k_lfilter_nf" in name:
+        return "lfilter_nf"
     if "k_pcm_batch" in name or "k_scale_batch" in name:
         return "pcm_batch"
     if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gc" in name:
@@ -47,6 +51,13 @@ def short(name):
 
 N_SIMD = 1024      # MI355X: 256 CUs x 4 SIMDs
 N_XCD = 8
+# GRBM_GUI_ACTIVE counts the GPU's busy cycles over the whole counter window,
+# which for a short dispatch includes the profiler's own time around it
+# (round 4 printed 5-8 GHz "clocks" for 6-30 us kernels): the derived clock and
+# VALU-busy share are reported only for dispatches of at least MIN_DERIVED_NS
+# and only when the clock is physical (<= MAX_CLOCK_GHZ; MI355X peaks at 2.4).
+MIN_DERIVED_NS = 50_000
+MAX_CLOCK_GHZ = 2.5
 
 
 def pass_durations(pass_dir):
@@ -92,11 +103,17 @@ def main(root, write=None):
         if "GRBM_GUI_ACTIVE" in c and grbm_dur.get(k):
             cycles = c["GRBM_GUI_ACTIVE"] / N_XCD
             dur = sum(grbm_dur[k]) / len(grbm_dur[k])
-            c["clock_ghz"] = cycles / dur
-            print(f"   effective clock             {c['clock_ghz']:.3f} GHz ({dur / 1e6:.4f} ms)")
-            if "SQ_ACTIVE_INST_VALU" in c:
-                c["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / cycles
-                print(f"   VALU-busy share of cycles   {c['valu_busy_frac']:.3f}")
+            clock = cycles / dur
+            if dur < MIN_DERIVED_NS or clock > MAX_CLOCK_GHZ:
+                c["clock_ghz"] = c["valu_busy_frac"] = "n/a"
+                print(f"   effective clock             n/a ({dur / 1e6:.4f} ms dispatch: "
+                      f"GRBM_GUI_ACTIVE spans more than the kernel, {clock:.2f} GHz)")
+            else:
+                c["clock_ghz"] = clock
+                print(f"   effective clock             {clock:.3f} GHz ({dur / 1e6:.4f} ms)")
+                if "SQ_ACTIVE_INST_VALU" in c:
+                    c["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / cycles
+                    print(f"   VALU-busy share of cycles   {c['valu_busy_frac']:.3f}")
         if "SQ_INSTS_VALU" in c and c.get("SQ_WAVES"):
             c["valu_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
             print(f"   VALU per wave               {c['valu_per_wave']:.1f}")
@@ -114,9 +131,9 @@ def main(root, write=None):
         data[wl] = {"channels": int(channels), "source": source,
                     "per_launch": {k: round(c["traffic_bytes"]) for k, c in out.items()
                                    if "traffic_bytes" in c},
-                    "derived": {k: {n: round(c[n], 4) for n in
-                                    ("clock_ghz", "valu_busy_frac", "valu_per_wave",
-                                     "lds_conflict_frac") if n in c}
+                    "derived": {k: {n: (round(c[n], 4) if isinstance(c[n], float) else c[n])
+                                    for n in ("clock_ghz", "valu_busy_frac", "valu_per_wave",
+                                              "lds_conflict_frac") if n in c}
                                 for k, c in out.items()}}
         with open(path, "w") as fh:
             json.dump(data, fh, indent=1)
