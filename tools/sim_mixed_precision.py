@@ -190,10 +190,199 @@ def df2t_model(y, sos, TS=48, p2_f32=(), clip=True):
     return np.clip(z, -1, 1) if clip else z
 
 
+def section_forms_model(y, sos, TS=48, forms=None, clip=True):
+    """z of one channel with pass 2 run per section in a chosen realisation and
+    precision, every sub-chunk restarting from the EXACT float64 state of that
+    realisation (what pass 1 + the float64 carry deliver; the kernel's
+    block-diagonal carry maps to any realisation's state by a fixed matrix).
+    forms[k] (default "df2"):
+      "df2"      float64 DF2, the shipped kernel (b0 pulled into the gain)
+      "df2_32"   DF2 in float32 (4 FMAs)
+      "df2t_32"  DF2 transposed in float32 (4 FMAs + 1 add)
+      "num32"    DF2 with the recursion w = u - a1 w1 - a2 w2 in float64 and
+                 the numerator y = w + c1 w1 + c2 w2 in float32 (w rounded)
+      "svf_32"   TPT state-variable filter (trapezoidal integrators, Simper's
+                 mixing y = m0 v0 + m1 v1 + m2 v2) in float32, 10 operations
+    (DF1 with error feedback was not modelled: the exact residual of a float32
+    recursion needs >= 9 float32 operations per section and sample, already
+    more issue time than the 4 float64 FMAs it would replace.)
+    """
+    rows, gain, norm = design.df2_realization(sos)
+    S = rows.shape[0]
+    forms = forms or {}
+    n = y.size
+    nsub = -(-n // TS)
+    ypad = np.zeros(nsub * TS, dtype=f32)
+    ypad[:n] = y
+    Y = ypad.reshape(nsub, TS)
+    svf = {}
+    for k in range(S):
+        if forms.get(k) == "svf_32":
+            _, c1, c2, a1, a2 = rows[k]
+            g2 = (1 + a1 + a2) / (1 - a1 + a2)
+            g = np.sqrt(g2)
+            D0 = 2 * (1 + g2) / (1 + a2)
+            gk = D0 - 1 - g2
+            kk = gk / g
+            # numerator of the section (DF2 row: 1, c1, c2 over 1, a1, a2) times D0
+            N = np.array([1.0, c1, c2]) * D0
+            Dz = np.array([1 + gk + g2, 2 * g2 - 2, 1 - gk + g2])
+            Mx = np.column_stack([Dz, g * np.array([1.0, 0.0, -1.0]), g2 * np.array([1.0, 2.0, 1.0])])
+            m = np.linalg.solve(Mx, N)
+            A1 = 1 / (1 + g * (g + kk))
+            svf[k] = (A1, g * A1, g * g * A1, m)
+    # exact float64 states per sub-chunk start, per section in its own form
+    def step64(k, u, st):
+        _, c1, c2, a1, a2 = rows[k]
+        f = forms.get(k, "df2")
+        if f in ("df2", "df2_32", "num32"):
+            w = u - a1 * st[0] - a2 * st[1]
+            yk = w + c1 * st[0] + c2 * st[1]
+            return yk, (w, st[0])
+        if f == "df2t_32":
+            yk = u + st[0]
+            return yk, (c1 * u - a1 * yk + st[1], c2 * u - a2 * yk)
+        if f == "svf_32":
+            A1, A2, A3, m = svf[k]
+            v3 = u - st[1]
+            v1 = A1 * st[0] + A2 * v3
+            v2 = st[1] + A2 * st[0] + A3 * v3
+            return m[0] * u + m[1] * v1 + m[2] * v2, (2 * v1 - st[0], 2 * v2 - st[1])
+        if f == "df1ef_32":  # DF1: state (x1, x2, y1, y2)
+            x1, x2, y1, y2 = st
+            yk = u + c1 * x1 + c2 * x2 - a1 * y1 - a2 * y2
+            return yk, (u, x1, yk, y1)
+        raise ValueError(f)
+    nst = [4 if forms.get(k) == "df1ef_32" else 2 for k in range(S)]
+    starts = [np.zeros((nsub, nst[k])) for k in range(S)]
+    st = [tuple([0.0] * nst[k]) for k in range(S)]
+    for l in range(nsub):
+        for k in range(S):
+            starts[k][l] = st[k]
+        for t in range(TS):
+            u = float(Y[l, t]) * gain
+            for k in range(S):
+                u, st[k] = step64(k, u, st[k])
+    out = np.zeros((nsub, TS))
+    cur = [[starts[k][:, i].copy() for i in range(nst[k])] for k in range(S)]
+    for k in range(S):
+        if forms.get(k, "df2").endswith("_32"):
+            cur[k] = [c.astype(f32) for c in cur[k]]
+    err = [np.zeros(nsub, dtype=f32) for _ in range(S)]
+    r32 = lambda v: np.asarray(v, np.float64).astype(f32)  # noqa: E731
+    for t in range(TS):
+        u = Y[:, t].astype(np.float64) * gain
+        for k in range(S):
+            _, c1, c2, a1, a2 = rows[k]
+            f = forms.get(k, "df2")
+            s = cur[k]
+            if f == "df2":
+                w = u - a1 * s[0] - a2 * s[1]
+                yk = w + c1 * s[0] + c2 * s[1]
+                cur[k] = [w, s[0]]
+            elif f == "num32":
+                w = u - a1 * s[0] - a2 * s[1]
+                w32, w1, w2 = r32(w), r32(s[0]), r32(s[1])
+                yk = fma32(f32(c2), w2, fma32(f32(c1), w1, w32)).astype(np.float64)
+                cur[k] = [w, s[0]]
+            elif f == "df2_32":
+                u32 = r32(u)
+                w = fma32(f32(-a2), s[1], fma32(f32(-a1), s[0], u32))
+                yk = fma32(f32(c2), s[1], fma32(f32(c1), s[0], w)).astype(np.float64)
+                cur[k] = [w, s[0]]
+            elif f == "df2t_32":
+                u32 = r32(u)
+                y32 = r32(u32.astype(np.float64) + s[0])
+                n1 = fma32(f32(c1), u32, fma32(f32(-a1), y32, s[1]))
+                n2 = fma32(f32(c2), u32, r32(f32(-a2) * y32))
+                cur[k] = [n1, n2]
+                yk = y32.astype(np.float64)
+            elif f == "svf_32":
+                A1, A2, A3, m = svf[k]
+                u32 = r32(u)
+                v3 = r32(u32.astype(np.float64) - s[1])
+                v1 = fma32(f32(A2), v3, r32(f32(A1) * s[0]))
+                v2 = fma32(f32(A3), v3, fma32(f32(A2), s[0], s[1]))
+                n1 = fma32(f32(2), v1, -s[0])
+                n2 = fma32(f32(2), v2, -s[1])
+                yk = fma32(f32(m[2]), v2, fma32(f32(m[1]), v1, r32(f32(m[0]) * u32))).astype(np.float64)
+                cur[k] = [n1, n2]
+            elif f == "df1ef_32":
+                u32 = r32(u)
+                x1, x2, y1, y2 = s
+                acc = fma32(f32(c2), x2, fma32(f32(c1), x1, u32))
+                acc = fma32(f32(-a2), y2, fma32(f32(-a1), y1, acc))
+                # first-order error feedback of the recursion's rounding
+                exact = (u32.astype(np.float64) + f32(c1) * x1.astype(np.float64)
+                         + f32(c2) * x2.astype(np.float64) - f32(a1) * y1.astype(np.float64)
+                         - f32(a2) * y2.astype(np.float64))
+                ykf = r32(acc.astype(np.float64) - f32(a1) * err[k].astype(np.float64))
+                err[k] = r32(ykf.astype(np.float64) - exact)
+                cur[k] = [u32, x1, ykf, y1]
+                yk = ykf.astype(np.float64)
+            u = yk
+        out[:, t] = u
+    z = out.reshape(-1)[:n].astype(f32)
+    return np.clip(z, -1, 1) if clip else z
+
+
+def section_table(channels=2):
+    """Per-section worst |dz| against the reference of every float32 form,
+    one section at a time (the others the shipped float64 DF2), over the
+    config-3 gains and eq.npz-style +-15 dB sets at 72 kHz, and config 5's
+    rate.  Printed as a markdown table."""
+    rng = np.random.default_rng(11)
+    cases = [
+        ("c3 @72k", 48000, 3, 2, None, orc.CONFIG3_GAINS),
+        ("+15 @72k", 48000, 3, 2, None, {b: 15 for b, _ in orc.BANDS}),
+        ("-15 @72k", 48000, 3, 2, None, {b: -15 for b, _ in orc.BANDS}),
+        ("+-15 @72k", 48000, 3, 2, None,
+         {b: (15 if i % 2 else -15) for i, (b, _) in enumerate(orc.BANDS)}),
+        ("-+15 @72k", 48000, 3, 2, None,
+         {b: (-15 if i % 2 else 15) for i, (b, _) in enumerate(orc.BANDS)}),
+        ("c5 @48k", 44100, 160, 147, 1023, orc.CONFIG3_GAINS),
+        ("+15 @48k", 44100, 160, 147, 1023, {b: 15 for b, _ in orc.BANDS}),
+    ]
+    forms = ["df2_32", "df2t_32", "num32", "svf_32"]
+    data = {}
+    for cname, fs, L, M, K, gains in cases:
+        xs = [rng.uniform(-1, 1, 48000).astype(np.float32) for _ in range(channels)]
+        refs = []
+        for x in xs:
+            yref, fs2 = orc.resample(x, fs, M, L, K)
+            refs.append((np.asarray(yref, dtype=np.float32), orc.equaliser(yref, fs2, gains), fs2))
+        sos = design.eq_plan(refs[0][2], gains).sos
+        base = max(float(np.max(np.abs(section_forms_model(y, sos) - zr))) for y, zr, _ in refs)
+        data[(cname, "fp64")] = base
+        for k in range(sos.shape[0]):
+            for f in forms:
+                e = max(float(np.max(np.abs(section_forms_model(y, sos, forms={k: f}) - zr)))
+                        for y, zr, _ in refs)
+                data[(cname, k, f)] = e
+        print(f"{cname}: fp64 {base:.2e}", flush=True)
+    names = [b for b, _ in orc.BANDS]
+    print("\n| section | form | " + " | ".join(c[0] for c in cases) + " | worst |")
+    print("|---|---|" + "---|" * (len(cases) + 1))
+    print("| all | float64 DF2 (shipped) | " + " | ".join(f"{data[(c[0], 'fp64')]:.1e}" for c in cases)
+          + f" | {max(data[(c[0], 'fp64')] for c in cases):.1e} |")
+    for k in range(6):
+        for f in forms:
+            vals = [data.get((c[0], k, f), float('nan')) for c in cases]
+            print(f"| {k} {names[k]} | {f} | " + " | ".join(f"{v:.1e}" for v in vals)
+                  + f" | {max(vals):.1e} |")
+    return data
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--channels", type=int, default=2)
+    ap.add_argument("--sections", action="store_true",
+                    help="per-section float32 realisations (DESIGN.md §3.0.7) instead of the "
+                         "round-3 variants")
     args = ap.parse_args()
+    if args.sections:
+        section_table(args.channels)
+        return
     rng = np.random.default_rng(7)
     cases = [
         ("c3 gains @72k", 48000, 3, 2, None, orc.CONFIG3_GAINS),
