@@ -80,22 +80,27 @@ inline int allow_lds(Kern kernel, size_t bytes) {
   return DSP_OK;
 }
 
-// Resident workgroups on the device for a kernel (asked once per calling thread and
-// kernel instance; thread_local: no state shared between threads).  The
-// kernel is a template argument so that every kernel has its own cache (as a
-// function argument, every instance of one signature shared it).
+// Resident workgroups on the device for a kernel (asked once per calling thread,
+// kernel instance and launch shape; thread_local: no state shared between
+// threads).  The kernel is a template argument so that every kernel has its
+// own cache (as a function argument, every instance of one signature shared
+// it); the cache is keyed by device, block size and LDS bytes (a kernel whose
+// LDS depends on the call's geometry asks again when it changes).
 template <auto K>
 int resident_groups(int threads, size_t shm) {
-  thread_local int dev = -1, cached = 0;
+  thread_local int dev = -1, cached = 0, cthreads = 0;
+  thread_local size_t cshm = 0;
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) return 0;
-  if (d != dev || cached <= 0) {
+  if (d != dev || cached <= 0 || threads != cthreads || shm != cshm) {
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(K),
                                                      threads, shm) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
       return 0;
     dev = d;
+    cthreads = threads;
+    cshm = shm;
     cached = per_cu * cus;
   }
   return cached;

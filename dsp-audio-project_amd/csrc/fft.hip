@@ -786,143 +786,181 @@ __device__ __forceinline__ int lane_now() {
   return l;
 }
 
-// No prefetch of the next frame.  (Holding the next frame in 64 more VGPRs,
-// 2 waves per SIMD, measured 0.199 vs 0.194 ms at config 4,
-// profiles/r03_spec_wave_oz_ab.jsonl.)  Round 4: a workgroup is a whole CU's
-// 16 waves sharing one LDS copy of the window (16 KB + 16 transpose buffers =
-// 151 KB), 4 waves per SIMD at <= 128 VGPRs (lane-derived values recomputed
-// per phase, twiddles loaded where used; 4 VGPRs spill, 20 B per lane); round
-// 3's 4-wave groups held the LDS to 3 groups = 3 waves per SIMD: 0.190 vs
-// 0.1955 ms at config 4, 0.0295 vs 0.030 at config 3 (profiles/r04_spec_ab.txt).
-__global__ __launch_bounds__(64 * kWavePerGroup) void k_spec_wave12(FftArgs a) {
+// One 4096-point transform t of the wave: raw = its frame's sample pairs
+// (wave_frame_load), wl0 = the window in LDS, buf = the wave's transpose
+// buffer.  Lane-derived values are recomputed (lane_now) in each phase
+// instead of held through it: 4 waves per SIMD need <= 128 VGPRs.
+__device__ __forceinline__ void w12_transform(const FftArgs& a, int64_t t, const u32x2_t (&raw)[32],
+                                              const pf2* wl0, float* buf) {
   constexpr int N = 4096, NH = 2048;
+  // (and of the window and twiddle addresses: hoisted, the window's 32 LDS
+  // reads hold 64 VGPRs and the twiddles ~20)
+  int z0 = 0;
+  asm volatile("" : "+s"(z0));
+  const pf2* win = wl0 + z0;
+  pf2 v[32];
+  const int l1 = lane_now();
+  // (the window's LDS reads in groups of 8: all 32 in flight would hold 64
+  // VGPRs beside the samples)
+#pragma unroll
+  for (int n1 = 0; n1 < 32; ++n1) {
+    if (n1 % 8 == 0) asm volatile("" ::: "memory");
+    v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} * win[64 * n1 + l1];
+  }
+  // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
+  // powers come from the table every 8 steps and by products in between)
+  pdft32(v, z0);
+  {
+    // the step's twiddles, loaded only now (live through the DFT above
+    // they cost ~10 VGPRs at its peak)
+    int z1 = 0;
+    asm volatile("" : "+s"(z1));
+    const pf2* twp = reinterpret_cast<const pf2*>(a.tw) + z1;
+    const int l2 = lane_now();
+    const pf2 wl = twp[2 * l2];               // W_2048^lane
+    pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const int m = (16 * l2 * k) & (N - 1);
+      w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
+    }
+    pf2 p = 0.5f * wl;
+    v[0] *= 0.5f;
+#pragma unroll
+    for (int k = 1; k < 32; ++k) {
+      if (k % 8 == 0) {
+        p = w8[k / 8 - 1];
+      } else if (k > 1) {
+        p = vcmul(p, wl);
+      }
+      v[k] = vcmul(v[k], p);
+    }
+  }
+  // T: Y[k1][n2] -> lane 2 k1 + h reads Y[k1][2m + h], one plane at a time
+  const int l3 = lane_now();
+  const int rd = (l3 >> 1) * kWaveRow + (l3 & 1);  // transpose read base
+  wave_lds_order();
+#pragma unroll
+  for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].x;
+  wave_lds_order();
+#pragma unroll
+  for (int m = 0; m < 32; ++m) v[m].x = buf[rd + 2 * m];
+  wave_lds_order();
+#pragma unroll
+  for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].y;
+  wave_lds_order();
+#pragma unroll
+  for (int m = 0; m < 32; ++m) v[m].y = buf[rd + 2 * m];
+  // B: DFT over m, then the radix-2 step across the lane pair: lane h = 1
+  // scales its F_1 by W_64^j, the pair swaps, and Z = own * (+-1) + other
+  pdft32(v, z0);
+  const int l4 = lane_now();
+  // (the lane's parity as an opaque float: the combine's 31 per-lane
+  // twiddles are loop-invariant, and hoisting them would hold 62 VGPRs)
+  const float hf = (float)(l4 & 1);
+  const pf2 hh = pf2{hf, hf};
+  const float sg = (l4 & 1) ? -1.f : 1.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    pf2 u = v[j];
+    if (j > 0) {
+      const pf2 one = pf2{1.f, 0.f};
+      u = vcmul(u, one + hh * (w128(2 * j, z0) - one));  // h ? W_64^j : 1
+    }
+    v[j] = u * sg + pf2{swap_pair(u.x), swap_pair(u.y)};
+  }
+  // real split and |X[K]|; W_4096^K = W_4096^K0 W_128^j
+  int z2 = 0;
+  asm volatile("" : "+s"(z2));
+  const int l5 = lane_now();
+  const int src = ((1 - l5) & 63) << 2;     // bpermute address of Z[-K]'s lane
+  const int K0 = (l5 >> 1) + 1024 * (l5 & 1);
+  const pf2 wb = (reinterpret_cast<const pf2*>(a.tw) + z2)[K0];  // W_4096^K0
+  float* mr = a.out + t * a.ld_out;
+  pf2 prev = v[0];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const pf2 q = pf2{bperm(src, v[31 - j].x), bperm(src, v[31 - j].y)};
+    const pf2 zm = l5 < 2 ? prev : q;
+    prev = q;
+    const pf2 zk = v[j];
+    const pf2 sm = pf2{zk.x + zm.x, zk.y - zm.y};
+    const pf2 d = pf2{zk.x - zm.x, zk.y + zm.y};
+    const pf2 x = vcfma(d, pw128(wb, j + 32, z0), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
+    mr[K0 + 32 * j] = cabsf_(make_float2(x.x, x.y));
+  }
+  if (l5 == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
+}
+
+// Round 4 (PF = 0): a workgroup is a whole CU's 16 waves sharing one LDS copy
+// of the window (16 KB + 16 transpose buffers = 151 KB), 4 waves per SIMD at
+// <= 128 VGPRs (lane-derived values recomputed per phase, twiddles loaded
+// where used; 4 VGPRs spill, 20 B per lane); no prefetch of the next frame
+// (round 3: holding it in 64 more VGPRs at 2 waves per SIMD measured 0.199 vs
+// 0.194 ms at config 4, profiles/r03_spec_wave_oz_ab.jsonl); round 3's 4-wave
+// groups held the LDS to 3 groups = 3 waves per SIMD: 0.190 vs 0.1955 ms at
+// config 4, 0.0295 vs 0.030 at config 3 (profiles/r04_spec_ab.txt).
+// PF = 1 (round 5 A/B): WPG waves per workgroup at 2 waves per SIMD, each with
+// its NEXT frame's loads in flight (64 more VGPRs) while it transforms the
+// current one: the loop runs two frames per iteration with the register sets'
+// roles swapped, so no copies.
+#ifndef DSP_SPEC_VARIANT
+#define DSP_SPEC_VARIANT 0
+#endif
+template <int WPG, int PF>
+__global__ __launch_bounds__(64 * WPG) void k_spec_w12(FftArgs a) {
+  constexpr int N = 4096;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the window, once per workgroup (LDS latency instead of an L2 round trip
   // per transform), then one transpose buffer per wave
-  for (int i = threadIdx.x; i < N / 4; i += 64 * kWavePerGroup)
+  for (int i = threadIdx.x; i < N / 4; i += 64 * WPG)
     reinterpret_cast<f32x4_t*>(ldsf)[i] = reinterpret_cast<const f32x4_t*>(a.win)[i];
   __syncthreads();
   const pf2* wl0 = reinterpret_cast<const pf2*>(ldsf);
   float* buf = ldsf + N + wv * kWaveLds;
-  // Lane-derived values are recomputed (lane_now) in each phase of the loop
-  // below instead of held through it: 4 waves per SIMD need <= 128 VGPRs.
-  const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
-  int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv;
-  u32x2_t raw[32];
-  for (; t < a.B; t += nw) {
-    wave_frame_load(a, t, lane_now(), raw);
-    // (and of the window and twiddle addresses: hoisted, the window's 32 LDS
-    // reads hold 64 VGPRs and the twiddles ~20)
-    int z0 = 0;
-    asm volatile("" : "+s"(z0));
-    const pf2* win = wl0 + z0;
-    pf2 v[32];
-    const int l1 = lane_now();
-    // (the window's LDS reads in groups of 8: all 32 in flight would hold 64
-    // VGPRs beside the samples)
-#pragma unroll
-    for (int n1 = 0; n1 < 32; ++n1) {
-      if (n1 % 8 == 0) asm volatile("" ::: "memory");
-      v[n1] = pf2{__uint_as_float(raw[n1][0]), __uint_as_float(raw[n1][1])} *
-              win[64 * n1 + l1];
+  const int64_t nw = (int64_t)gridDim.x * WPG;
+  int64_t t = (int64_t)blockIdx.x * WPG + wv;
+  if constexpr (PF == 0) {
+    u32x2_t raw[32];
+    for (; t < a.B; t += nw) {
+      wave_frame_load(a, t, lane_now(), raw);
+      w12_transform(a, t, raw, wl0, buf);
     }
-    // A: DFT over n1, then W_2048^(lane k1) / 2 (W_2048^m = W_4096^(2m); the
-    // powers come from the table every 8 steps and by products in between)
-    pdft32(v, z0);
-    {
-      // the step's twiddles, loaded only now (live through the DFT above
-      // they cost ~10 VGPRs at its peak)
-      int z1 = 0;
-      asm volatile("" : "+s"(z1));
-      const pf2* twp = reinterpret_cast<const pf2*>(a.tw) + z1;
-      const int l2 = lane_now();
-      const pf2 wl = twp[2 * l2];               // W_2048^lane
-      pf2 w8[3];                                // W_2048^(8 lane k) / 2, k = 1..3
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        const int m = (16 * l2 * k) & (N - 1);
-        w8[k - 1] = (m < NH ? 0.5f : -0.5f) * twp[m & (NH - 1)];
-      }
-      pf2 p = 0.5f * wl;
-      v[0] *= 0.5f;
-#pragma unroll
-      for (int k = 1; k < 32; ++k) {
-        if (k % 8 == 0) {
-          p = w8[k / 8 - 1];
-        } else if (k > 1) {
-          p = vcmul(p, wl);
-        }
-        v[k] = vcmul(v[k], p);
-      }
+  } else {
+    u32x2_t ra[32], rb[32];
+    if (t < a.B) wave_frame_load(a, t, lane_now(), ra);
+    for (; t < a.B; t += 2 * nw) {
+      if (t + nw < a.B) wave_frame_load(a, t + nw, lane_now(), rb);
+      w12_transform(a, t, ra, wl0, buf);
+      if (t + nw >= a.B) break;
+      if (t + 2 * nw < a.B) wave_frame_load(a, t + 2 * nw, lane_now(), ra);
+      w12_transform(a, t + nw, rb, wl0, buf);
     }
-    // T: Y[k1][n2] -> lane 2 k1 + h reads Y[k1][2m + h], one plane at a time
-    const int l3 = lane_now();
-    const int rd = (l3 >> 1) * kWaveRow + (l3 & 1);  // transpose read base
-    wave_lds_order();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].x;
-    wave_lds_order();
-#pragma unroll
-    for (int m = 0; m < 32; ++m) v[m].x = buf[rd + 2 * m];
-    wave_lds_order();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) buf[k * kWaveRow + l3] = v[k].y;
-    wave_lds_order();
-#pragma unroll
-    for (int m = 0; m < 32; ++m) v[m].y = buf[rd + 2 * m];
-    // B: DFT over m, then the radix-2 step across the lane pair: lane h = 1
-    // scales its F_1 by W_64^j, the pair swaps, and Z = own * (+-1) + other
-    pdft32(v, z0);
-    const int l4 = lane_now();
-    // (the lane's parity as an opaque float: the combine's 31 per-lane
-    // twiddles are loop-invariant, and hoisting them would hold 62 VGPRs)
-    const float hf = (float)(l4 & 1);
-    const pf2 hh = pf2{hf, hf};
-    const float sg = (l4 & 1) ? -1.f : 1.f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      pf2 u = v[j];
-      if (j > 0) {
-        const pf2 one = pf2{1.f, 0.f};
-        u = vcmul(u, one + hh * (w128(2 * j, z0) - one));  // h ? W_64^j : 1
-      }
-      v[j] = u * sg + pf2{swap_pair(u.x), swap_pair(u.y)};
-    }
-    // real split and |X[K]|; W_4096^K = W_4096^K0 W_128^j
-    int z2 = 0;
-    asm volatile("" : "+s"(z2));
-    const int l5 = lane_now();
-    const int src = ((1 - l5) & 63) << 2;     // bpermute address of Z[-K]'s lane
-    const int K0 = (l5 >> 1) + 1024 * (l5 & 1);
-    const pf2 wb = (reinterpret_cast<const pf2*>(a.tw) + z2)[K0];  // W_4096^K0
-    float* mr = a.out + t * a.ld_out;
-    pf2 prev = v[0];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const pf2 q = pf2{bperm(src, v[31 - j].x), bperm(src, v[31 - j].y)};
-      const pf2 zm = l5 < 2 ? prev : q;
-      prev = q;
-      const pf2 zk = v[j];
-      const pf2 sm = pf2{zk.x + zm.x, zk.y - zm.y};
-      const pf2 d = pf2{zk.x - zm.x, zk.y + zm.y};
-      const pf2 x = vcfma(d, pw128(wb, j + 32, z0), sm);  // s - i W d  (-i W_128^j = W_128^(j+32))
-      mr[K0 + 32 * j] = cabsf_(make_float2(x.x, x.y));
-    }
-    if (l5 == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
   }
 }
 
-int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
-  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
-  if (int rc = allow_lds(k_spec_wave12, shm)) return rc;
-  const int res = resident_groups<k_spec_wave12>(64 * kWavePerGroup, shm);
+template <int WPG, int PF>
+int launch_w12(const FftArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)(4096 + WPG * kWaveLds) * sizeof(float);
+  if (int rc = allow_lds(k_spec_w12<WPG, PF>, shm)) return rc;
+  const int res = resident_groups<k_spec_w12<WPG, PF>>(64 * WPG, shm);
   DSP_REQUIRE(res > 0, "occupancy query failed");
-  const int64_t groups = ceil_div(a.B, kWavePerGroup);
+  const int64_t groups = ceil_div(a.B, WPG);
   const unsigned grid = (unsigned)(groups < res ? groups : res);
-  hipLaunchKernelGGL(k_spec_wave12, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
+  hipLaunchKernelGGL((k_spec_w12<WPG, PF>), dim3(grid), dim3(64 * WPG), shm, s, a);
   DSP_LAUNCHED("k_spec_wave12");
   return DSP_OK;
+}
+
+int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+#if DSP_SPEC_VARIANT == 1
+  return launch_w12<8, 1>(a, s);
+#elif DSP_SPEC_VARIANT == 2
+  return launch_w12<4, 1>(a, s);
+#else
+  return launch_w12<kWavePerGroup, 0>(a, s);
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -12,7 +12,11 @@ reference names, argument order and meaning (dsp_core.py:10,41,68,104,133,179,
 * 2-D numpy [B, n] in -> the same, per row (batched; the reference cannot take
   2-D signals, so this extends rather than changes its contract); from
   SHARD_MIN_ROWS rows on a node with several GPUs the rows are sharded over
-  all of them (bitwise the one-GPU result);
+  all of them (bitwise the one-GPU result) -- only in a single-process
+  program on device 0: with torch.distributed initialised, or another current
+  device (a rank that picked its GPU with set_device), every call stays on the
+  current device; DSPCORE_SHARD=0 / 1 in the environment turns sharding off /
+  on regardless;
 * a ROCm torch tensor ([n] or [B, n]) in -> a device tensor out, float32 /
   complex64, left on the GPU with no synchronisation.
 
@@ -141,8 +145,20 @@ def _run(x, fn, np_dtype, complex_ok=False):
 
 
 def _shard_devices():
-    """The devices a large 2-D numpy batch is sharded over: every visible GPU."""
+    """The devices a large 2-D numpy batch is sharded over: every visible GPU,
+    unless this looks like one rank of a multi-process job (torch.distributed
+    initialised, or a current device other than 0), which must keep to its own
+    GPU; DSPCORE_SHARD=0 / 1 overrides."""
+    import os
+
     import torch
+    env = os.environ.get("DSPCORE_SHARD", "")
+    if env == "0":
+        return []
+    if env != "1":
+        import torch.distributed as tdist
+        if (tdist.is_available() and tdist.is_initialized()) or torch.cuda.current_device() != 0:
+            return []
     return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
 
 

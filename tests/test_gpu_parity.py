@@ -763,6 +763,24 @@ def test_drop_in_shards_large_batches(gpu, monkeypatch):
     assert got
 
 
+def test_drop_in_sharding_stays_on_a_ranks_device(gpu, monkeypatch):
+    """_shard_devices: every visible GPU in a single-process program on device
+    0; none (the call stays on the current device) once torch.distributed is
+    initialised, as in one rank of a multi-process job; DSPCORE_SHARD=0 / 1
+    overrides either way."""
+    import torch.distributed as tdist
+    dc = _dc()
+    monkeypatch.delenv("DSPCORE_SHARD", raising=False)
+    assert len(dc._shard_devices()) == torch.cuda.device_count()
+    monkeypatch.setattr(tdist, "is_initialized", lambda: True)
+    assert dc._shard_devices() == []
+    monkeypatch.setenv("DSPCORE_SHARD", "1")
+    assert len(dc._shard_devices()) == torch.cuda.device_count()
+    monkeypatch.setenv("DSPCORE_SHARD", "0")
+    monkeypatch.setattr(tdist, "is_initialized", lambda: False)
+    assert dc._shard_devices() == []
+
+
 def test_shards_plan_with_the_job_batch(gpu):
     """Two-launch geometry (config 5's L/M = 160/147), 4096 rows: planned with
     the job's batch (Chain(plan_batch=4096)) every shard of 1, 2 and 4 runs the
