@@ -1285,7 +1285,7 @@ __device__ __forceinline__ int64_t gen_window_start(const TileArgs& a, int64_t t
 // Steps 1-5 of one tile of k_chain_gct for one wave whose x window x[qa ..]
 // is in `win` (REPAIR: the rerun with the non-finite path; entry:
 // tile_cascade's).
-template <int L, int M, bool T7, bool REPAIR, class ENTRY = ChainedEntry>
+template <int L, int M, bool T7, bool REPAIR, int G = 2, class ENTRY = ChainedEntry>
 __device__ __forceinline__ void gct_tile(const TileArgs& a, const float* seq, float* win,
                                          int lane, int64_t b, int64_t tile, int64_t qa,
                                          ENTRY&& entry = ENTRY{}) {
@@ -1312,12 +1312,12 @@ __device__ __forceinline__ void gct_tile(const TileArgs& a, const float* seq, fl
     f32x2 X[NPW];
 #pragma unroll
     for (int m = 0; m < NPW; ++m) X[m] = f32x2{xl[2 * m], xl[2 * m + 1]};
-    // Outputs in pairs, the next pair's tap rows read while this one computes
-    // and the two FMA chains interleaved (each output's own chain, pairs in
-    // ascending order, is unchanged: y bitwise the same).  Against one output
-    // at a time: 1.128 -> 1.122 ms at config 5 (profiles/r04_gct_pairs_ab.txt);
-    // groups of 4 spill.
-    constexpr int G = 2;
+    // Outputs in groups of G, the next group's tap rows read while this one
+    // computes and the G FMA chains interleaved (each output's own chain,
+    // groups in ascending order, is unchanged: y bitwise the same).  G = 2
+    // against one output at a time: 1.128 -> 1.122 ms at config 5
+    // (profiles/r04_gct_pairs_ab.txt); groups of 4 spill at 4 waves per SIMD
+    // and pay at the persistent kernel's 3 (profiles/r05_gcp_ab.txt).
     static_assert(kGenTS % G == 0, "whole groups");
     struct Row {
       f32x4 t0, t1;
@@ -1423,48 +1423,69 @@ __global__ __launch_bounds__(kWave * kGenWaves) void k_chain_gct_repair(TileArgs
 // another workgroup).  Every tile's end state is still published for the
 // repair kernel.  Rows are bitwise the chained kernel's: the same tile code on
 // the same entry states.  Config 5 (8192 channels): 1.134-1.137 vs
-// 1.191-1.200 ms same box (profiles/r04_gcp_ab.txt).  Issuing part of the next
-// tile's window behind pass 2 (registers) measured the same with 2 of its 8
-// float4 per lane and slower with 4 (spills): not kept.
+// 1.191-1.200 ms same box (profiles/r04_gcp_ab.txt).
+// Round 5: 3 waves per SIMD (up to 168 VGPRs) instead of 4, which buys (a) the
+// next tile's x window in flight in registers behind the whole current tile
+// -- loaded as soon as this tile's window is in LDS, the next channel's tile 0
+// behind a channel's last tile -- and (b) the SRC in groups of 4 outputs:
+// 1.116 -> 1.094 ms same box (profiles/r05_gcp_ab.txt; (a) alone 1.098).  At 4
+// waves per SIMD half the window in flight measured the same and the whole
+// window spilled (round 4); an LDS-DMA into a second window slot does not fit
+// the LDS, and stores straight from registers instead of store_tile's LDS
+// staging, which would free the slot, ran 1.6x (default cache policy) to 6x
+// (nt) slower (16-byte pieces 128 bytes apart).
 constexpr int kGcpWin = 8;  // float4 per lane of a tile's x window (a.win <= 4 * 8 * 64)
 
 template <int L, int M, bool T7 = false>
-__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(3))) void
 k_chain_gcp(TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = gen_wave();
-  const int lane = threadIdx.x & (kWave - 1);
   const int64_t groups = (a.B + kGenWaves - 1) / kGenWaves;
   float* seq = smem;
   ct_load_classes(a, seq);
   float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
   const int nf = a.win >> 2;
+  f32x4 v[kGcpWin];
+  auto load = [&](int64_t bb, int64_t tile) {
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + bb * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    const int64_t qa = gen_window_start<L, M>(a, tile);
+    const int ln = lane_id();
+#pragma unroll
+    for (int r = 0; r < kGcpWin; ++r)  // past the window: harmless reads
+      v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * (r * kWave + ln)) * 4), 0,
+                                                   kStream);
+  };
+  if ((int64_t)blockIdx.x * kGenWaves + w < a.B) load((int64_t)blockIdx.x * kGenWaves + w, 0);
   for (int64_t g = blockIdx.x; g < groups; g += gridDim.x) {
     const int64_t b = g * kGenWaves + w;
     if (b >= a.B) break;  // the last group's missing channels (wave-uniform)
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
     RegCarry carry{0.0, 0.0};
     for (int64_t tile = 0; tile < a.ntiles; ++tile) {
       const int64_t qa = gen_window_start<L, M>(a, tile);
-      f32x4 v[kGcpWin];
+      {
+        const int ln = lane_id();
 #pragma unroll
-      for (int r = 0; r < kGcpWin; ++r)  // past the window: harmless reads
-        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)((qa + 4 * (r * kWave + lane)) * 4),
-                                                     0, kStream);
-#pragma unroll
-      for (int r = 0; r < kGcpWin; ++r) {
-        // (rows r < kGcpWin - 1 are whole: the launcher checks nf; one exec
-        // mask instead of eight held through the loop)
-        const int f = r * kWave + lane;
-        if (r < kGcpWin - 1 || f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+        for (int r = 0; r < kGcpWin; ++r) {
+          // (rows r < kGcpWin - 1 are whole: the launcher checks nf; one exec
+          // mask instead of eight)
+          const int f = r * kWave + ln;
+          if (r < kGcpWin - 1 || f < nf) *reinterpret_cast<f32x4*>(win + 4 * f) = v[r];
+        }
       }
       fence();
+      if (tile + 1 < a.ntiles) {
+        load(b, tile + 1);
+      } else {
+        const int64_t bn = b + (int64_t)gridDim.x * kGenWaves;
+        if (bn < a.B) load(bn, 0);
+      }
       // (an opaque lane per tile: what the tile derives from it is recomputed
       // instead of hoisted out of the loop and held through it)
       int ln = lane_id();
       asm volatile("" : "+v"(ln));
-      gct_tile<L, M, T7, false>(a, seq, win, ln, b, tile, qa, carry);
+      gct_tile<L, M, T7, false, 4>(a, seq, win, ln, b, tile, qa, carry);
     }
   }
 }

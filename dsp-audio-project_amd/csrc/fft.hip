@@ -892,75 +892,47 @@ __device__ __forceinline__ void w12_transform(const FftArgs& a, int64_t t, const
   if (l5 == 0) mr[NH] = 2.f * fabsf(v[0].x - v[0].y);  // X[N/2] = Re Z[0] - Im Z[0]
 }
 
-// Round 4 (PF = 0): a workgroup is a whole CU's 16 waves sharing one LDS copy
-// of the window (16 KB + 16 transpose buffers = 151 KB), 4 waves per SIMD at
-// <= 128 VGPRs (lane-derived values recomputed per phase, twiddles loaded
-// where used; 4 VGPRs spill, 20 B per lane); no prefetch of the next frame
-// (round 3: holding it in 64 more VGPRs at 2 waves per SIMD measured 0.199 vs
-// 0.194 ms at config 4, profiles/r03_spec_wave_oz_ab.jsonl); round 3's 4-wave
-// groups held the LDS to 3 groups = 3 waves per SIMD: 0.190 vs 0.1955 ms at
-// config 4, 0.0295 vs 0.030 at config 3 (profiles/r04_spec_ab.txt).
-// PF = 1 (round 5 A/B): WPG waves per workgroup at 2 waves per SIMD, each with
-// its NEXT frame's loads in flight (64 more VGPRs) while it transforms the
-// current one: the loop runs two frames per iteration with the register sets'
-// roles swapped, so no copies.
-#ifndef DSP_SPEC_VARIANT
-#define DSP_SPEC_VARIANT 0
-#endif
-template <int WPG, int PF>
-__global__ __launch_bounds__(64 * WPG) void k_spec_w12(FftArgs a) {
+// A workgroup is a whole CU's 16 waves sharing one LDS copy of the window
+// (16 KB + 16 transpose buffers = 151 KB), 4 waves per SIMD at <= 128 VGPRs
+// (lane-derived values recomputed per phase, twiddles loaded where used; 4
+// VGPRs spill, 20 B per lane); round 3's 4-wave groups held the LDS to 3
+// groups = 3 waves per SIMD: 0.190 vs 0.1955 ms at config 4, 0.0295 vs 0.030
+// at config 3 (profiles/r04_spec_ab.txt).  Measured and not adopted: the next
+// frame in flight in 64 more VGPRs (2 waves per SIMD): 0.211 vs 0.193 ms at
+// config 4 (round 3: 0.199 vs 0.194; profiles/r05_spec_pf_ab.txt); the waves
+// of a SIMD starting 0.25 .. 1.5 us apart (round 5) or 4 .. 12 us apart (round
+// 4): neutral / slower.  The memory-only floor of this launch (frame loads
+// and |X| stores, no transform) is 0.166 ms at config 4 and 22.6 us at config
+// 3, against 0.194 / 0.0305 ms with the transform (profiles/r05_spec_floor.txt).
+__global__ __launch_bounds__(64 * kWavePerGroup) void k_spec_wave12(FftArgs a) {
   constexpr int N = 4096;
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the window, once per workgroup (LDS latency instead of an L2 round trip
   // per transform), then one transpose buffer per wave
-  for (int i = threadIdx.x; i < N / 4; i += 64 * WPG)
+  for (int i = threadIdx.x; i < N / 4; i += 64 * kWavePerGroup)
     reinterpret_cast<f32x4_t*>(ldsf)[i] = reinterpret_cast<const f32x4_t*>(a.win)[i];
   __syncthreads();
   const pf2* wl0 = reinterpret_cast<const pf2*>(ldsf);
   float* buf = ldsf + N + wv * kWaveLds;
-  const int64_t nw = (int64_t)gridDim.x * WPG;
-  int64_t t = (int64_t)blockIdx.x * WPG + wv;
-  if constexpr (PF == 0) {
-    u32x2_t raw[32];
-    for (; t < a.B; t += nw) {
-      wave_frame_load(a, t, lane_now(), raw);
-      w12_transform(a, t, raw, wl0, buf);
-    }
-  } else {
-    u32x2_t ra[32], rb[32];
-    if (t < a.B) wave_frame_load(a, t, lane_now(), ra);
-    for (; t < a.B; t += 2 * nw) {
-      if (t + nw < a.B) wave_frame_load(a, t + nw, lane_now(), rb);
-      w12_transform(a, t, ra, wl0, buf);
-      if (t + nw >= a.B) break;
-      if (t + 2 * nw < a.B) wave_frame_load(a, t + 2 * nw, lane_now(), ra);
-      w12_transform(a, t + nw, rb, wl0, buf);
-    }
+  const int64_t nw = (int64_t)gridDim.x * kWavePerGroup;
+  u32x2_t raw[32];
+  for (int64_t t = (int64_t)blockIdx.x * kWavePerGroup + wv; t < a.B; t += nw) {
+    wave_frame_load(a, t, lane_now(), raw);
+    w12_transform(a, t, raw, wl0, buf);
   }
 }
 
-template <int WPG, int PF>
-int launch_w12(const FftArgs& a, hipStream_t s) {
-  const size_t shm = (size_t)(4096 + WPG * kWaveLds) * sizeof(float);
-  if (int rc = allow_lds(k_spec_w12<WPG, PF>, shm)) return rc;
-  const int res = resident_groups<k_spec_w12<WPG, PF>>(64 * WPG, shm);
+int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)(4096 + kWavePerGroup * kWaveLds) * sizeof(float);
+  if (int rc = allow_lds(k_spec_wave12, shm)) return rc;
+  const int res = resident_groups<k_spec_wave12>(64 * kWavePerGroup, shm);
   DSP_REQUIRE(res > 0, "occupancy query failed");
-  const int64_t groups = ceil_div(a.B, WPG);
+  const int64_t groups = ceil_div(a.B, kWavePerGroup);
   const unsigned grid = (unsigned)(groups < res ? groups : res);
-  hipLaunchKernelGGL((k_spec_w12<WPG, PF>), dim3(grid), dim3(64 * WPG), shm, s, a);
+  hipLaunchKernelGGL(k_spec_wave12, dim3(grid), dim3(64 * kWavePerGroup), shm, s, a);
   DSP_LAUNCHED("k_spec_wave12");
   return DSP_OK;
-}
-
-int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
-#if DSP_SPEC_VARIANT == 1
-  return launch_w12<8, 1>(a, s);
-#elif DSP_SPEC_VARIANT == 2
-  return launch_w12<4, 1>(a, s);
-#else
-  return launch_w12<kWavePerGroup, 0>(a, s);
-#endif
 }
 
 // ---------------------------------------------------------------------------
