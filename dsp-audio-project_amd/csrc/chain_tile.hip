@@ -373,17 +373,21 @@ __device__ __forceinline__ void src_part(const float* xw, tt_ptr tt, float (&y)[
   }
 }
 
-// LDS float of output float g = 4 (lane + 64 k) in store_tile's staging,
-// g + 4 (g div TS) (row stride TS + 4), as a per-lane base plus a constant:
-//   TS = 32: 4 lane + 4 (lane >> 3) + 288 k (one base);
-//   TS = 48: (lane + 64 k) div 12 = a + [k >= 3] + [r + 4 (k mod 3) >= 12]
-//            with lane = 12 a + r, so three bases, by k mod 3, and 276 k + 4 [k >= 3].
+// LDS float of output float g = 4 (lane + 64 k) in store_tile's staging, as a
+// per-lane base plus a constant:
+//   TS = 32 (round 5): row stride 32 with the float4 column XOR-swizzled by
+//            the row's low 3 bits: row r = g div 32 = lane div 8 + 8 k, column
+//            4 ((lane mod 8) ^ (r mod 8)) = 4 ((lane mod 8) ^ (lane div 8 mod
+//            8)): one base and 256 k;
+//   TS = 48: g + 4 (g div TS) (row stride TS + 4): (lane + 64 k) div 12 = a +
+//            [k >= 3] + [r + 4 (k mod 3) >= 12] with lane = 12 a + r, so three
+//            bases, by k mod 3, and 276 k + 4 [k >= 3].
 template <int TS>
 struct StageBase {
   int b[3];
   __device__ __forceinline__ explicit StageBase(int lane) {
     if constexpr (TS == 32) {
-      b[0] = 4 * lane + 4 * (lane >> 3);
+      b[0] = 32 * (lane >> 3) + 4 * ((lane & 7) ^ ((lane >> 3) & 7));
     } else {
       static_assert(TS == 48, "staging rows of 8 or 12 float4s");
       const int a = (lane * 43) >> 9;  // lane div 12 (lane < 64)
@@ -394,25 +398,28 @@ struct StageBase {
     }
   }
   __device__ __forceinline__ int at(int k) const {
-    if constexpr (TS == 32) return b[0] + 288 * k;
+    if constexpr (TS == 32) return b[0] + 256 * k;
     else return b[k % 3] + 276 * k + (k >= 3 ? 4 : 0);
   }
 };
 
 // Stores the tile's 64 x TS outputs (lane l holds outputs l*TS + i) as
 // coalesced float4s through `rs`, a buffer resource whose base is the tile's
-// first output: each half of the lanes writes its rows into LDS (row stride
-// TS + 4: conflict-free ds_write_b128), then all 64 lanes store the half's
-// contiguous 32*TS floats.  The resource checks every dword: stores past the
-// row's end are dropped, a float4 across it keeps its head.
-// (The reads take 2-way bank conflicts in some ds_read_b128 lane groups, 48
-// cycles per call at TS = 48; an XOR-swizzled unpadded layout free of them
-// cost more in the VALU that computes its addresses than the LDS cycles it
-// saved: chain 5.73-5.77 vs 5.68-5.70 ms at config 4, same box, round 4.)
+// first output: each half of the lanes writes its rows into LDS, then all 64
+// lanes store the half's contiguous 32*TS floats.  The resource checks every
+// dword: stores past the row's end are dropped, a float4 across it keeps its
+// head.  TS = 48 (config 3/4): row stride TS + 4, conflict-free ds_write_b128;
+// the reads take 2-way bank conflicts in some ds_read_b128 lane groups, 48
+// cycles per call; an XOR-swizzled unpadded layout free of them cost more in
+// the VALU that computes its addresses than the LDS cycles it saved there
+// (chain 5.73-5.77 vs 5.68-5.70 ms at config 4, same box, round 4: that kernel
+// is VALU-issue-bound at the power cap).  TS = 32 (round 5): the swizzle of
+// StageBase, free of conflicts both ways (tools/ldsmodel.py --ts32: the padded
+// layout's reads took 32 extra cycles per call) for 8 VALU per call.
 template <int TS>
 __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int lane,
                                            __amdgpu_buffer_rsrc_t rs) {
-  constexpr int RS = TS + 4;
+  constexpr int RS = TS == 32 ? 32 : TS + 4;
   constexpr int NF4 = (kWave / 2) * TS / 4;
   static_assert(NF4 % kWave == 0, "whole float4 rounds per half");
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -422,9 +429,10 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
     fence();
     if ((lane >> 5) == h) {
       float* row = lds + (lane & 31) * RS;
+      const int sw = TS == 32 ? (lane & 7) : 0;  // the row's column swizzle
 #pragma unroll
       for (int k = 0; k < TS / 4; ++k)
-        *reinterpret_cast<float4*>(row + 4 * k) =
+        *reinterpret_cast<float4*>(row + 4 * (k ^ sw)) =
             make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
     fence();

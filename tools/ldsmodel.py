@@ -10,6 +10,7 @@ The model reproduced round 3's PMC exactly (SQ_LDS_BANK_CONFLICT / SQ_WAVES =
 in store_tile's staging reads.
 
     python tools/ldsmodel.py [--round3]
+    python tools/ldsmodel.py --ts32       (config 5's TS = 32 kernels)
 """
 import sys
 
@@ -79,7 +80,63 @@ def model(round3=False):
     return tot
 
 
+def ex_b32(addr, active=ALL):
+    """ds_read_b32 (and each half of ds_read2_b32): 2 groups of 32 lanes,
+    banks (a/4) mod 32."""
+    e = 0
+    for g in (range(0, 32), range(32, 64)):
+        banks = {}
+        for lane in g:
+            if lane in active:
+                a = addr(lane)
+                banks.setdefault(a % 32, set()).add(a)
+        e += max((len(v) for v in banks.values()), default=1) - 1
+    return e
+
+
+def model_ts32(L=160, M=147, T=7, c=511, tiles=4):
+    """The TS = 32 kernels at config 5's 160/147 (k_chain_gct / k_chain_gcp),
+    per tile and wave: the SRC's window pair reads (19 ds_read2_b32, lane
+    offsets ~29.4 floats apart) and store_tile's staging for y and z, padded
+    (round 4: row stride 36) and XOR-swizzled (round 5: stride 32, float4
+    column ^ row mod 8)."""
+    tot = {}
+
+    def add(name, v):
+        tot[name] = tot.get(name, 0) + v / tiles
+    for tile in range(tiles):
+        m0 = tile * 2048
+        qa = ((m0 * M + c) // L - (T - 1)) // 4 * 4
+
+        def o(lane):
+            return (m0 * M + c + 32 * M * lane) // L - (T - 1) - qa
+        for m in range(19):
+            add("window pair reads", ex_b32(lambda l, m=m: o(l) + 2 * m)
+                + ex_b32(lambda l, m=m: o(l) + 2 * m + 1))
+        for h in range(2):
+            half = {lane for lane in ALL if (lane >> 5) == h}
+            for k in range(8):
+                add("padded staging writes", 2 * extra("w128", lambda l, k=k: (l & 31) * 36 + 4 * k, half))
+                add("swizzled staging writes",
+                    2 * extra("w128", lambda l, k=k: 32 * (l & 31) + 4 * (k ^ (l & 7)), half))
+            for k in range(4):
+                def padded(lane, k=k):
+                    g = 4 * (lane + 64 * k)
+                    return (g // 32) * 36 + g % 32
+
+                def swz(lane, k=k):
+                    row = lane // 8 + 8 * k
+                    return 32 * row + 4 * ((lane % 8) ^ (row & 7))
+                add("padded staging reads", 2 * extra("r128", padded))
+                add("swizzled staging reads", 2 * extra("r128", swz))
+    return tot
+
+
 if __name__ == "__main__":
+    if "--ts32" in sys.argv:
+        for name, v in model_ts32().items():
+            print(f"{name:26s} {v:.1f} extra cycles per tile and wave")
+        sys.exit(0)
     tot = model("--round3" in sys.argv)
     for name, v in tot.items():
         print(f"{name:22s} {v}")
