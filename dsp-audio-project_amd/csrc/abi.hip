@@ -79,7 +79,8 @@ int dsp_version(void) {
   // 2.4.0: inf / NaN through the FFT and spectrum entry points get the
   // reference's labels (fft_nf.hip); dsp_fft_workspace_bytes adds the
   // four-step's per-row header; dsp_lfilter_nonfinite_f32 (round 5).
-  return 20400;
+  // 2.5.0: DSP_MAX_LOG2N_FFT 28 -> 30 (nested four-step, round 5).
+  return 20500;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }

@@ -262,8 +262,8 @@ struct NfArgs {
 int launch_nf_small(const NfArgs& a, hipStream_t s);
 // log2n > DSP_MAX_LOG2N, B <= 65535 rows: hdr (2 words per row: flag set by the
 // four-step's first step, list length, both zeroed before it), lists (row r's
-// at lists + r * list_stride words, >= N words each).
-int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint32_t* lists, int64_t list_stride,
+// at lists + r * list_stride 64-bit entries, >= N entries each).
+int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint64_t* lists, int64_t list_stride,
                     hipStream_t s);
 size_t biquad_workspace_bytes(int64_t B, int64_t n, int S, int64_t chunk_len);
 // lfilter's non-finite labels after the cascade (lfilter_nf.hip).

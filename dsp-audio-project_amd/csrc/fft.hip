@@ -962,8 +962,49 @@ struct Fft4Args {
   FftArgs a;          // in / out / rows / segment / window / W_N table
   float2* ws;         // B x N complex
   int64_t N;          // NA * NB
-  uint32_t* hdr;      // per row: non-finite flag, list length (fft_nf.hip)
+  uint32_t* hdr;      // per row: non-finite flag, list length (fft_nf.hip); NULL: none
+  int64_t tws = 1;    // a.tw is the table of N * tws points (nested inner steps)
+  int64_t nest = 0;   // step B of a nested inner transform: the outer NA (run_fft6_row)
+  const float2* twc = nullptr;  // N * tws > 2^20: W^(i << tsh), i < (N * tws) >> tsh
+  int tsh = 0;
 };
+
+// The inter-step twiddle W_Nt^m, Nt = N * tws.  Up to 2^20 points one read of
+// the caller's table; above, W^m = W^(hi << tsh) W^lo with lo < 2^tsh, tsh =
+// ceil(log2 Nt / 2): the fine factor from the table's first 2^tsh entries, the
+// coarse one from the 2^(log2 Nt - tsh) entries k_tw_coarse gathered into the
+// workspace -- both contiguous and L2-resident, where the workgroup's W^(n1 k2)
+// alone are scattered over the whole table (one line fetched per 8-byte
+// twiddle: round 5 measured the 2^28 four-step at 0.49 TB/s).  One more
+// rounding (~1 ulp of 1), far inside the FFT's 1e-5.
+__device__ __forceinline__ float2 tw_step(const Fft4Args& f, int64_t m) {
+  const int64_t Nt = f.N * f.tws;
+  if (!f.twc) return tw_full(f.a.tw, m, Nt);
+  m &= Nt - 1;
+  const float2 a = f.twc[m >> f.tsh], b = f.a.tw[m & ((int64_t(1) << f.tsh) - 1)];
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__global__ __launch_bounds__(256) void k_tw_coarse(const float2* __restrict__ tw, float2* twc,
+                                                   int64_t N, int tsh) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (N >> tsh)) twc[i] = tw_full(tw, i << tsh, N);
+}
+
+// Four-step sizes whose twiddles go through the coarse table, its shift and
+// its size in bytes.
+constexpr int kLog2TwSplit = 20;
+inline int tw_shift(int log2n) { return (log2n + 1) / 2; }
+inline size_t tw_coarse_bytes(int log2n) {
+  return log2n > kLog2TwSplit ? (size_t(1) << (log2n - tw_shift(log2n))) * sizeof(float2) : 0;
+}
+int build_tw_coarse(const float2* tw, float2* twc, int log2n, hipStream_t s) {
+  const int64_t n = int64_t(1) << (log2n - tw_shift(log2n));
+  hipLaunchKernelGGL(k_tw_coarse, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, tw, twc,
+                     int64_t(1) << log2n, tw_shift(log2n));
+  DSP_LAUNCHED("k_tw_coarse");
+  return DSP_OK;
+}
 
 // Step A's input: a non-finite value sets `nf` (the row's flag for the
 // non-finite repair, fft_nf.hip) and, for the complex transforms, reads as
@@ -999,17 +1040,23 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
   const FftArgs& a = f.a;
   const int64_t NB = f.N / NA;
   const int64_t b = blockIdx.y;
-  const int64_t c0 = (int64_t)blockIdx.x * KC;
+  // XCD-aware: the workgroups the dispatcher sends to one XCD (every 8th) take
+  // consecutive column groups, so the two 64-byte halves of a 128-byte line
+  // are fetched into the same L2
+  int64_t gx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) gx = (gx & 7) * (gridDim.x >> 3) + (gx >> 3);
+  const int64_t c0 = gx * KC;
   const InRow ir = in_row<MODE>(a, b);
   bool nf = false;
   for (int i = threadIdx.x; i < KC * NA; i += NT) {
     const int c = i % KC, n2 = i / KC;
-    lds[c * TS + lpad(n2)] = load_input_nf<MODE>(a, ir, (int)(c0 + c + NB * n2), nf);
+    const int n = (int)(c0 + c + NB * n2);
+    lds[c * TS + lpad(n2)] = f.hdr ? load_input_nf<MODE>(a, ir, n, nf) : load_input<MODE>(a, ir, n, true);
   }
   if (nf) f.hdr[2 * b] = 1u;
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2A, 0> tw;
-  load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA);
+  load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA * f.tws);
   __syncthreads();
   run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
   __syncthreads();
@@ -1017,10 +1064,14 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
   for (int i = threadIdx.x; i < KC * NA; i += NT) {
     const int c = i % KC, k2 = i / KC;
     const int64_t n1 = c0 + c;
-    y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], tw_full(a.tw, n1 * k2, f.N));
+    y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], tw_step(f, n1 * k2 * f.tws));
   }
 }
 
+// Step B.  Nested (run_fft6_row, f.nest = the outer NA): the KC rows of a
+// workgroup are one inner row r = blockIdx.x of KC consecutive outer rows k2 =
+// blockIdx.y KC + c, so that the natural-order output k of (k2, r), X[k2 +
+// nest k], is written in runs of KC consecutive addresses.
 template <int LOG2B, int MODE>
 __global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
   using PL = Plan<LOG2B>;
@@ -1029,27 +1080,46 @@ __global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const FftArgs& a = f.a;
   const int64_t NA = f.N / NB;
-  const int64_t b = blockIdx.y;
-  const int64_t r0 = (int64_t)blockIdx.x * KC;  // first k2 row
-  const float2* y = f.ws + b * f.N;
+  // source row of lane group c: ws + src0 + c * src_c; output k1 of it at
+  // out0 + c * out_c + k1 * out_k (complex / magnitude units)
+  int64_t src0, src_c, out0, out_c, out_k;
+  if (f.nest) {
+    const int64_t k2 = (int64_t)blockIdx.y * KC, r = blockIdx.x;
+    src0 = k2 * f.N + r * NB;
+    src_c = f.N;
+    out0 = k2 + f.nest * r;
+    out_c = 1;
+    out_k = f.nest * NA;
+  } else {
+    const int64_t b = blockIdx.y, r0 = (int64_t)blockIdx.x * KC;  // first k2 row
+    src0 = b * f.N + r0 * NB;
+    src_c = NB;
+    out0 = b * a.ld_out + r0;
+    out_c = 1;
+    out_k = NA;
+  }
+  const float2* y = f.ws + src0;
   for (int i = threadIdx.x; i < KC * NB; i += NT) {
     const int r = i / NB, n1 = i - r * NB;
-    lds[r * TS + lpad(n1)] = y[(r0 + r) * NB + n1];
+    lds[r * TS + lpad(n1)] = y[r * src_c + n1];
   }
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2B, 0> tw;
-  load_tw<LOG2B, 0>(tw, a.tw, j0, f.N / NB);
+  load_tw<LOG2B, 0>(tw, a.tw, j0, f.N / NB * f.tws);
   __syncthreads();
   run_pass<LOG2B, 0>(LdsIO<NB>{lds + tl * TS}, lds + tl * TS, j0, tw);
   __syncthreads();
+  // the spectrum keeps k <= N_outer / 2 (row-relative index: out - row base)
+  const int64_t onh = f.N * (f.nest ? f.nest : 1) / 2;
+  const int64_t rel0 = f.nest ? out0 : out0 - (int64_t)blockIdx.y * a.ld_out;
   for (int i = threadIdx.x; i < KC * NB; i += NT) {
     const int c = i % KC, k1 = i / KC;
-    const int64_t k = r0 + c + NA * k1;
+    const int64_t d = c * out_c + k1 * out_k;
     const float2 v = lds[c * TS + lpad(k1)];
     if constexpr (MODE == kSpec) {
-      if (k <= f.N / 2) a.out[b * a.ld_out + k] = cabsf_(v);
+      if (rel0 + d <= onh) a.out[out0 + d] = cabsf_(v);
     } else {
-      reinterpret_cast<float2*>(a.out)[b * a.ld_out + k] = v;
+      reinterpret_cast<float2*>(a.out)[out0 + d] = v;
     }
   }
 }
@@ -1092,6 +1162,88 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
     case 27: return launch_fft4<13, 14, MODE>(f, s);  // (one column per 2^14 workgroup:
     case 28: return launch_fft4<14, 14, MODE>(f, s);  //  strided, not coalesced, loads)
     default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
+  }
+}
+
+// Three-pass (nested) four-step from N = 2^DSP_FFT_NEST_FROM up to 2^30
+// (round 5; the reference's recursion has no size limit, dsp_core.py:41-66):
+// N = NA * NB with NB = NB1 * NB2 and all three at most 2^10 (so every
+// sub-transform moves 8 columns -- 64 B runs -- per HBM access; the two-step
+// split of 2^24 and up needs sub-transforms of 2^12..2^14, 4..1 columns):
+//   step A   (k_fft4_a<LA>): the NB columns of NA points of the row, the
+//            twiddle W_N^(n1 k2) on the way out -> Y[k2][n1] (rows of NB);
+//   step A'  (k_fft4_a<LA1>, complex): the NA rows' columns of NB1 points
+//            with W_NB = W_N^NA (table stride tws = NA) -> Y'[k2][..];
+//   step B'  (k_fft4_b<LB2>, nest = NA): rows of NB2 points, 8 outer rows k2
+//            per workgroup, natural-order output k of row k2 -> X[k2 + NA k].
+// One row at a time (the workspace is 2 N complex whatever B).
+// (From 2^25: the two-pass split's 2^12..2^14-point sub-transforms move 4..1
+// columns per access; round 5 measured 0.684 vs 0.715 ms at 2^25, 5.98 vs
+// 9.90 ms at 2^28, and the two-pass faster at 2^24, 0.290 vs 0.313 ms --
+// profiles/r05_fft_large.txt.)
+#ifndef DSP_FFT_NEST_FROM
+#define DSP_FFT_NEST_FROM 25
+#endif
+constexpr int kLog2Nested = DSP_FFT_NEST_FROM;
+static_assert(kLog2Nested > DSP_MAX_LOG2N + 1 && kLog2Nested <= DSP_MAX_LOG2N_FFT, "nest from");
+
+template <int LA, int LA1, int LB2, int MODE>
+int run_fft6_row(const FftArgs& row, float2* Y, float2* Y2, const float2* twc, uint32_t* hdr,
+                 hipStream_t s) {
+  constexpr int64_t N = int64_t(1) << (LA + LA1 + LB2);
+  constexpr int64_t NA = int64_t(1) << LA, NB = N / NA;
+  constexpr int KA = kcols_for(LA), K1 = kcols_for(LA1), KB = kcols_for(LB2);
+  static_assert(KA == kCols && K1 == kCols && KB == kCols && NA % KB == 0, "3-pass split");
+  using PA = Plan<LA>;
+  using P1 = Plan<LA1>;
+  using PB = Plan<LB2>;
+  const size_t sa = (size_t)KA * (PA::PADN + 1) * sizeof(float2);
+  const size_t s1 = (size_t)K1 * (P1::PADN + 1) * sizeof(float2);
+  const size_t sb = (size_t)KB * (PB::PADN + 1) * sizeof(float2);
+  if (int rc = allow_lds(k_fft4_a<LA, MODE>, sa)) return rc;
+  if (int rc = allow_lds(k_fft4_a<LA1, kC2C>, s1)) return rc;
+  if (int rc = allow_lds(k_fft4_b<LB2, MODE>, sb)) return rc;
+  Fft4Args fa{row, Y, N, hdr};
+  fa.twc = twc;
+  fa.tsh = tw_shift(LA + LA1 + LB2);
+  hipLaunchKernelGGL((k_fft4_a<LA, MODE>), dim3((unsigned)(NB / KA), 1), dim3(KA * PA::TPT), sa, s,
+                     fa);
+  DSP_LAUNCHED("k_fft4_a");
+  // the inner transforms over the NA rows of Y: complex in, W_NB from the W_N
+  // table at stride NA
+  const FftArgs inner{reinterpret_cast<const float*>(Y), row.out, NA, NB, row.ld_out, 0, 0, 0, 1,
+                      nullptr, row.tw};
+  Fft4Args f1{inner, Y2, NB, nullptr};
+  f1.tws = NA;
+  f1.twc = twc;
+  f1.tsh = fa.tsh;
+  hipLaunchKernelGGL((k_fft4_a<LA1, kC2C>), dim3((unsigned)((NB >> LA1) / K1), (unsigned)NA),
+                     dim3(K1 * P1::TPT), s1, s, f1);
+  DSP_LAUNCHED("k_fft4_a");
+  Fft4Args fb = f1;
+  fb.nest = NA;
+  hipLaunchKernelGGL((k_fft4_b<LB2, MODE>), dim3((unsigned)(NB >> LB2), (unsigned)(NA / KB)),
+                     dim3(KB * PB::TPT), sb, s, fb);
+  DSP_LAUNCHED("k_fft4_b");
+  return DSP_OK;
+}
+
+template <int MODE>
+int dispatch6(const FftArgs& row, int log2n, float2* Y, float2* Y2, const float2* twc,
+              uint32_t* hdr, hipStream_t s) {
+  switch (log2n) {
+    case 20: return run_fft6_row<6, 7, 7, MODE>(row, Y, Y2, twc, hdr, s);
+    case 21: return run_fft6_row<7, 7, 7, MODE>(row, Y, Y2, twc, hdr, s);
+    case 22: return run_fft6_row<7, 7, 8, MODE>(row, Y, Y2, twc, hdr, s);
+    case 23: return run_fft6_row<7, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
+    case 24: return run_fft6_row<8, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
+    case 25: return run_fft6_row<8, 8, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    case 26: return run_fft6_row<8, 9, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    case 27: return run_fft6_row<9, 9, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    case 28: return run_fft6_row<9, 9, 10, MODE>(row, Y, Y2, twc, hdr, s);
+    case 29: return run_fft6_row<9, 10, 10, MODE>(row, Y, Y2, twc, hdr, s);
+    case 30: return run_fft6_row<10, 10, 10, MODE>(row, Y, Y2, twc, hdr, s);
+    default: return set_error(DSP_EINVAL, "log2n=%d outside the three-pass range", log2n);
   }
 }
 
@@ -1245,12 +1397,17 @@ namespace {
 constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
 }  // namespace
 
-// [Y: B x N complex][non-finite header: 2 words per row of a launch part]
+// Two-pass sizes: [Y: B x N complex][coarse twiddles][non-finite header: 2
+// words per row of a launch part].  Three-pass (run_fft6_row, one row at a
+// time): [Y: N][Y': N complex][coarse twiddles][header: 2 words per row].
+// The coarse twiddle table (tw_step) above 2^20 points: 2^floor(log2n / 2)
+// complex.
 size_t fft_workspace_bytes(int64_t B, int log2n) {
   if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
-  const size_t rows = (size_t)(B < kMaxRows4 ? B : kMaxRows4);
-  return add_sat(mul_sat((size_t)B, (size_t)1 << log2n, sizeof(float2)),
-                 mul_sat(rows, 2, sizeof(uint32_t)));
+  const bool three = log2n >= kLog2Nested;
+  const size_t rows = three ? (size_t)B : (size_t)(B < kMaxRows4 ? B : kMaxRows4);
+  const size_t data = mul_sat(three ? 2 : (size_t)B, (size_t)1 << log2n, sizeof(float2));
+  return add_sat(add_sat(data, tw_coarse_bytes(log2n)), mul_sat(rows, 2, sizeof(uint32_t)));
 }
 
 namespace {
@@ -1264,20 +1421,46 @@ int run_fft4(FftArgs a, int log2n, void* ws, size_t ws_bytes, hipStream_t s) {
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 7) == 0, "FFT workspace not 8-byte aligned");
   const int64_t B = a.B;
   const int64_t N = int64_t(1) << log2n;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + (size_t)B * N * 8);
+  if (log2n >= kLog2Nested) {
+    float2* Y = static_cast<float2*>(ws);
+    float2* twc = Y + 2 * N;
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(twc + tw_coarse_bytes(log2n) / sizeof(float2));
+    if (int rc = build_tw_coarse(a.tw, twc, log2n, s)) return rc;
+    DSP_HIP(hipMemsetAsync(hdr, 0, (size_t)B * 2 * sizeof(uint32_t), s));
+    for (int64_t b = 0; b < B; ++b) {
+      FftArgs row = a;
+      row.B = 1;
+      row.in = a.in + b * a.ld_in * (MODE == kC2C ? 2 : 1);
+      row.out = a.out + b * a.ld_out * (MODE == kSpec ? 1 : 2);
+      if (int rc = dispatch6<MODE>(row, log2n, Y, Y + N, twc, hdr + 2 * b, s)) return rc;
+      const NfArgs nfa{row.in, row.out, 1, row.ld_in, row.ld_out, row.seg_start, row.seg_len,
+                       row.hop, row.frames, row.win, reinterpret_cast<const float*>(row.tw), MODE,
+                       log2n};
+      if (int rc = launch_nf_large(nfa, hdr + 2 * b, reinterpret_cast<uint64_t*>(Y), N, s))
+        return rc;
+    }
+    return DSP_OK;
+  }
+  float2* twc = tw_coarse_bytes(log2n) ? static_cast<float2*>(ws) + B * N : nullptr;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + (size_t)B * N * 8 +
+                                              tw_coarse_bytes(log2n));
+  if (twc)
+    if (int rc = build_tw_coarse(a.tw, twc, log2n, s)) return rc;
   for (int64_t b0 = 0; b0 < B; b0 += kMaxRows4) {
     FftArgs part = a;
     part.B = B - b0 < kMaxRows4 ? B - b0 : kMaxRows4;
     part.in = a.in + b0 * a.ld_in * (MODE == kC2C ? 2 : 1);
     part.out = a.out + b0 * a.ld_out * (MODE == kSpec ? 1 : 2);
     DSP_HIP(hipMemsetAsync(hdr, 0, (size_t)part.B * 2 * sizeof(uint32_t), s));
-    const Fft4Args f{part, static_cast<float2*>(ws), N, hdr};
+    Fft4Args f{part, static_cast<float2*>(ws), N, hdr};
+    f.twc = twc;
+    f.tsh = tw_shift(log2n);
     if (int rc = dispatch4<MODE>(f, log2n, s)) return rc;
     // the rows' non-finite inputs, listed in the freed Y rows
     const NfArgs nfa{part.in, part.out, part.B, part.ld_in, part.ld_out, part.seg_start,
                      part.seg_len, part.hop, part.frames, part.win,
                      reinterpret_cast<const float*>(part.tw), MODE, log2n};
-    if (int rc = launch_nf_large(nfa, hdr, static_cast<uint32_t*>(ws), 2 * N, s)) return rc;
+    if (int rc = launch_nf_large(nfa, hdr, static_cast<uint64_t*>(ws), N, s)) return rc;
   }
   return DSP_OK;
 }

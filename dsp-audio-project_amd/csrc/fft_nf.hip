@@ -71,15 +71,17 @@ __device__ __forceinline__ float2 nf_input(const NfArgs& a, int64_t t, int64_t n
 }
 
 // Packed list entry of input n with component classes (cr, ci), or 0 when
-// both are finite (n < 2^28: 28 bits of index, 2 + 2 of class).
-__device__ __forceinline__ uint32_t nf_entry(int64_t n, float2 v) {
+// both are finite: index << 4 | cr << 2 | ci (32-bit entries in k_nf_small's
+// LDS, n < 2^14; 64-bit in the four-step's workspace lists, n < 2^30).
+template <typename E>
+__device__ __forceinline__ E nf_entry(int64_t n, float2 v) {
   const int cr = nf_code(v.x), ci = nf_code(v.y);
-  return (cr | ci) ? ((uint32_t)n << 4) | (uint32_t)(cr << 2) | (uint32_t)ci : 0u;
+  return (cr | ci) ? ((E)n << 4) | (E)(cr << 2) | (E)ci : E(0);
 }
 
 // The class pair that input entry e contributes to X[k] (see the header).
-__device__ __forceinline__ float2 nf_path(uint32_t e, uint32_t k, int lg) {
-  const uint32_t n = e >> 4;
+__device__ __forceinline__ float2 nf_path(uint64_t e, uint32_t k, int lg) {
+  const uint32_t n = (uint32_t)(e >> 4);
   float cr = nf_cls((e >> 2) & 3), ci = nf_cls(e & 3);
 #pragma unroll 1
   for (int l = 1; l <= lg; ++l) {
@@ -101,8 +103,8 @@ __device__ __forceinline__ float2 nf_path(uint32_t e, uint32_t k, int lg) {
 }
 
 // Class-sum over the list for output k (stops once both components are NaN).
-__device__ __forceinline__ float2 nf_classes(const uint32_t* list, uint32_t count, uint32_t k,
-                                             int lg) {
+template <typename E>
+__device__ __forceinline__ float2 nf_classes(const E* list, uint32_t count, uint32_t k, int lg) {
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll 1
   for (uint32_t i = 0; i < count; ++i) {
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(kNfThreads) void k_nf_small(NfArgs a) {
     if (tid == 0) counts[1] = 0;
     __syncthreads();
     for (uint32_t n = tid; n < N; n += kNfThreads) {
-      const uint32_t e = nf_entry(n, nf_input(a, t, n));
+      const uint32_t e = nf_entry<uint32_t>(n, nf_input(a, t, n));
       if (e) list[atomicAdd(&counts[1], 1u)] = e;
     }
     __syncthreads();
@@ -211,28 +213,28 @@ __global__ __launch_bounds__(kNfThreads) void k_nf_small(NfArgs a) {
 
 // Above DSP_MAX_LOG2N.  hdr[2 r] = row r's flag (set by the four-step's first
 // step), hdr[2 r + 1] = its list length; the list of row r is
-// lists[r * list_stride ...].
-__global__ __launch_bounds__(kNfThreads) void k_nf_list(NfArgs a, uint32_t* hdr, uint32_t* lists,
+// lists[r * list_stride ...] (64-bit entries).
+__global__ __launch_bounds__(kNfThreads) void k_nf_list(NfArgs a, uint32_t* hdr, uint64_t* lists,
                                                         int64_t list_stride) {
   const int64_t r = blockIdx.y;
   if (!hdr[2 * r]) return;
   const int64_t N = int64_t(1) << a.log2n;
-  uint32_t* list = lists + r * list_stride;
+  uint64_t* list = lists + r * list_stride;
   for (int64_t n = (int64_t)blockIdx.x * kNfThreads + threadIdx.x; n < N;
        n += (int64_t)gridDim.x * kNfThreads) {
-    const uint32_t e = nf_entry(n, nf_input(a, r, n));
+    const uint64_t e = nf_entry<uint64_t>(n, nf_input(a, r, n));
     if (e) list[atomicAdd(&hdr[2 * r + 1], 1u)] = e;
   }
 }
 
 __global__ __launch_bounds__(kNfThreads) void k_nf_fix(NfArgs a, const uint32_t* hdr,
-                                                       const uint32_t* lists, int64_t list_stride) {
+                                                       const uint64_t* lists, int64_t list_stride) {
   const int64_t r = blockIdx.y;
   const uint32_t cnt = hdr[2 * r + 1];
   if (!hdr[2 * r] || !cnt) return;
   const int64_t N = int64_t(1) << a.log2n;
   const int64_t nout = a.mode == 2 ? N / 2 + 1 : N;
-  const uint32_t* list = lists + r * list_stride;
+  const uint64_t* list = lists + r * list_stride;
   for (int64_t k = (int64_t)blockIdx.x * kNfThreads + threadIdx.x; k < nout;
        k += (int64_t)gridDim.x * kNfThreads)
     nf_store(a, r, (uint32_t)k, nf_classes(list, cnt, (uint32_t)k, a.log2n));
@@ -253,7 +255,7 @@ int launch_nf_small(const NfArgs& a, hipStream_t s) {
   return DSP_OK;
 }
 
-int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint32_t* lists, int64_t list_stride,
+int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint64_t* lists, int64_t list_stride,
                     hipStream_t s) {
   DSP_REQUIRE(a.log2n > DSP_MAX_LOG2N && a.log2n <= DSP_MAX_LOG2N_FFT,
               "non-finite repair: log2n=%d", a.log2n);
@@ -267,7 +269,7 @@ int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint32_t* lists, int64_t lis
                      list_stride);
   DSP_LAUNCHED("k_nf_list");
   hipLaunchKernelGGL(k_nf_fix, dim3(gl, (unsigned)a.B), dim3(kNfThreads), 0, s, a,
-                     static_cast<const uint32_t*>(hdr), static_cast<const uint32_t*>(lists),
+                     static_cast<const uint32_t*>(hdr), static_cast<const uint64_t*>(lists),
                      list_stride);
   DSP_LAUNCHED("k_nf_fix");
   return DSP_OK;

@@ -29,7 +29,7 @@ DSP_EHIP = -2
 DSP_ENOTSUP = -3
 DSP_MAX_STAGES = 16
 DSP_MAX_LOG2N = 14
-DSP_MAX_LOG2N_FFT = 28
+DSP_MAX_LOG2N_FFT = 30
 DSP_MAX_DFT = 8192
 DSP_LFILTER_NF_MAX = 4096
 

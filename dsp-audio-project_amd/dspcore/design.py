@@ -446,9 +446,10 @@ def hann(n: int) -> np.ndarray:
         return 0.5 - 0.5 * np.cos(2 * np.pi * k / (n - 1))
 
 
-def twiddles(n: int) -> np.ndarray:
-    """exp(-2j pi k / N), k < N/2, computed in float64 (dsp_core.py:59-60)."""
-    k = np.arange(max(n // 2, 1))
+def twiddles(n: int, start: int = 0, stop: int | None = None) -> np.ndarray:
+    """exp(-2j pi k / N), start <= k < stop (default N/2), computed in float64
+    (dsp_core.py:59-60)."""
+    k = np.arange(start, max(n // 2, 1) if stop is None else stop)
     return np.exp(-2j * np.pi * k / n)
 
 

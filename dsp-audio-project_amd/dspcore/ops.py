@@ -62,8 +62,13 @@ def _table(kind: str, n: int, device: torch.device) -> torch.Tensor:
     def build():
         if kind == "hann":
             host = hann(n).astype(np.float32)
-        else:
-            host = twiddles(n).astype(np.complex64).view(np.float32)
+        else:  # in slices: 2^29 float64 twiddles at once would hold ~24 GB of host temporaries
+            half = max(n // 2, 1)
+            host = np.empty(half, dtype=np.complex64)
+            for k0 in range(0, half, 1 << 22):
+                k1 = min(half, k0 + (1 << 22))
+                host[k0:k1] = twiddles(n, k0, k1)
+            host = host.view(np.float32)
         return torch.from_numpy(np.ascontiguousarray(host)).to(device)
     return _cached((kind, n, device.index), build)
 

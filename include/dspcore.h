@@ -37,7 +37,7 @@ extern "C" {
 
 #define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
-#define DSP_MAX_LOG2N_FFT 28 /* largest FFT / spectrum (four-step above 2^14)  */
+#define DSP_MAX_LOG2N_FFT 30 /* largest FFT / spectrum (four-step above 2^14)  */
 #define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
 #define DSP_LFILTER_NF_MAX 4096 /* largest order dsp_lfilter_nonfinite_f32 takes */
 
@@ -127,10 +127,13 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
  * complex elements).  `out` is interleaved complex [B][ld_out].  `twiddles` is
  * the interleaved complex table exp(-2*pi*i*k/N), k < N/2, in float32.
  * Up to DSP_MAX_LOG2N one launch keeps each transform in LDS and needs no
- * workspace; above it a four-step transform (two launches) keeps its
- * intermediate in `workspace` (device, 8-byte aligned,
- * >= dsp_fft_workspace_bytes(B, log2n) = B * N * 8 bytes plus a header of 8
- * bytes per row (at most 65535 rows); 0 below).
+ * workspace; above it a four-step transform keeps its intermediate in
+ * `workspace` (device, 8-byte aligned, >= dsp_fft_workspace_bytes(B, log2n);
+ * 0 below): up to 2^24 two launches over all rows, B * N * 8 bytes; from 2^25
+ * (ABI 2.5, up to 2^30) three launches (a four-step nested in step B) row by
+ * row, 2 * N * 8 bytes whatever B; plus, above 2^20, a coarse twiddle table of
+ * 2^floor(log2n / 2) * 8 bytes, and a header of 8 bytes per row (per launch
+ * part of at most 65535 rows for two launches).
  * Non-finite input (ABI 2.4): every output component gets the class --
  * finite, +inf, -inf or NaN -- that the reference's recursive radix-2 DIT in
  * complex128 numpy arithmetic gives it (inf * 0 = NaN at the k = 0 twiddles,

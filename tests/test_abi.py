@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20400     # 2.4.0: FFT/spectrum non-finite repair (2.3.0: chain variants)
+    assert lib.dsp_version() == 20500     # 2.5.0: FFT to 2^30 (2.4.0: FFT/spectrum non-finite repair)
     assert isinstance(_lib.last_error(), str)
 
 
@@ -26,16 +26,22 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     lib = _lib.load()
     rc = lib.dsp_src_polyphase_f32(None, None, 1, 10, 10, 10, 10, None, 121, 0, 2, 0, None)
     assert rc == _lib.DSP_EINVAL and "L=0" in _lib.last_error()
-    rc = lib.dsp_fft_c2c_f32(None, None, 1, 29, 1, 1 << 29, 1 << 29, None, None, 0, None)
+    rc = lib.dsp_fft_c2c_f32(None, None, 1, 31, 1, 1 << 31, 1 << 31, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL
-    # four-step sizes need a workspace of B * N complex plus the non-finite
-    # header, 8 bytes per row of a launch part (<= 65535 rows)
+    # four-step sizes: the two-pass split (2^15..2^24) needs B * N complex, the
+    # three-pass one (2^25..2^30, row by row) 2 N complex; above 2^20 the
+    # coarse twiddle table, 2^floor(log2n / 2) complex; then the non-finite
+    # header, 8 bytes per row (of a launch part of <= 65535 rows: two-pass)
     assert lib.dsp_fft_workspace_bytes(3, 14) == 0
     assert lib.dsp_fft_workspace_bytes(3, 15) == 3 * (1 << 15) * 8 + 3 * 8
-    assert lib.dsp_fft_workspace_bytes(3, 26) == 3 * (1 << 26) * 8 + 3 * 8
-    assert lib.dsp_fft_workspace_bytes(1, 28) == (1 << 28) * 8 + 8
-    assert lib.dsp_fft_workspace_bytes(1, 29) == 0
-    assert lib.dsp_fft_workspace_bytes(3, 27) == 3 * (1 << 27) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(2, 22) == 2 * (1 << 22) * 8 + (1 << 11) * 8 + 2 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 24) == 3 * (1 << 24) * 8 + (1 << 12) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 25) == 2 * (1 << 25) * 8 + (1 << 12) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 26) == 2 * (1 << 26) * 8 + (1 << 13) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(1, 28) == 2 * (1 << 28) * 8 + (1 << 14) * 8 + 8
+    assert lib.dsp_fft_workspace_bytes(1, 29) == 2 * (1 << 29) * 8 + (1 << 14) * 8 + 8
+    assert lib.dsp_fft_workspace_bytes(5, 30) == 2 * (1 << 30) * 8 + (1 << 15) * 8 + 5 * 8
+    assert lib.dsp_fft_workspace_bytes(1, 31) == 0
     assert lib.dsp_fft_workspace_bytes(70000, 15) == 70000 * (1 << 15) * 8 + 65535 * 8
     rc = lib.dsp_fft_c2c_f32(1024, 1024, 1, 15, 1, 1 << 15, 1 << 15, 1024, None, 0, None)
     assert rc == _lib.DSP_EINVAL and "workspace" in _lib.last_error()

@@ -816,8 +816,8 @@ def test_fft_four_step_matches_reference(gpu):
     """N = 2^13 .. 2^16 through the drop-in against the reference's own outputs
     (tests/golden/fft_large.npz; 2^15 and 2^16 take the four-step path), and
     2^17 .. 2^22 batched and 2^23 / 2^24 / 2^26 against np.fft.fft, 2^27 and
-    2^28 against the exact DFT of a sum of tones: max|dX| <= 1e-5 * max|X|;
-    2^29 raises RuntimeError."""
+    2^28 against the exact DFT of a sum of tones: max|dX| <= 1e-5 * max|X|
+    (2^29 and 2^30: test_fft_nested_four_step)."""
     dc = _dc()
     g = golden("fft_large")
     for k in (13, 14, 15, 16):
@@ -874,8 +874,82 @@ def test_fft_four_step_matches_reference(gpu):
         assert err <= FFT_RTOL * n * 0.75, (lg, err)
         del X, want
         torch.cuda.empty_cache()
+
+
+def _tones(n, f, amp, gpu, real=False):
+    """sum_j amp_j exp(2 pi i f_j t / n) (or its real part, cos tones) on the
+    device, phases reduced mod n in int64 and formed in float64."""
+    idx = torch.arange(n, dtype=torch.int64, device=gpu)
+    x = torch.zeros(n, dtype=torch.float32 if real else torch.complex64, device=gpu)
+    for fj, aj in zip(f, amp):
+        ph = ((fj * idx) % n).double() * (2 * np.pi / n)
+        if real:
+            x += (aj * torch.cos(ph)).float()
+        else:
+            x += (aj * torch.polar(torch.ones_like(ph), ph)).to(torch.complex64)
+        del ph
+    return x
+
+
+def test_fft_nested_four_step(gpu):
+    """2^29 and 2^30 (round 5, the nested four-step of csrc/fft.hip run_fft6_row;
+    the reference's recursion has no size cap, dsp_core.py:41-66): sums of
+    tones against their exact DFT (max|dX| <= 1e-5 * max|X|), two complex rows
+    at 2^29 and a real row at 2^30; the 2^29 spectrum against |FFT| of the same
+    windowed float32 row; an inf at n = 0 (every X[k].real +inf, X.imag the
+    DFT of the rest) and in the spectrum's segment (every bin non-finite);
+    2^31 raises RuntimeError."""
+    ops = _ops()
+    n = 1 << 29
+    f = [[3, 777777, n // 3, n - 5], [1, 2, n // 2, n - 1]]
+    amp = [[0.5, -0.25 + 0.5j, 0.75j, 0.3], [0.25, 0.5, -0.5, 0.125j]]
+    x = torch.stack([_tones(n, f[r], amp[r], gpu) for r in range(2)])
+    X = ops.fft(x)
+    for r in range(2):
+        want = torch.zeros(n, dtype=torch.complex64, device=gpu)
+        want[torch.tensor(f[r], device=gpu)] = torch.tensor(
+            [n * a for a in amp[r]], dtype=torch.complex64, device=gpu)
+        err = float(torch.max(torch.abs(X[r] - want)))
+        assert err <= FFT_RTOL * n * 0.75, (r, err)
+        del want
+    # an inf at n = 0 rides every output's real part unchanged (W^0 = 1)
+    xz = x[:1].clone()
+    xz[0, 0] = complex(0.0, x[0, 0].imag.item())
+    x[0, 0] = complex(np.inf, x[0, 0].imag.item())
+    Xi = ops.fft(x[:1])
+    Xz = ops.fft(xz)
+    assert bool(torch.all(torch.isposinf(Xi.real)))
+    assert torch.equal(Xi.imag, Xz.imag)
+    del x, X, Xi, Xz, xz
+    torch.cuda.empty_cache()
+    # the 2^29 spectrum: centre segment shorter than N (zero padded)
+    xr = _tones(n, [12345, n // 7], [0.5, 0.25], gpu, real=True)
+    mag = ops.spectrum(xr[None, :], 1000, n - 5000, n)[0]
+    seg = torch.zeros(n, dtype=torch.float32, device=gpu)
+    seg[:n - 5000] = xr[1000:n - 4000]
+    seg *= ops._table("hann", n, torch.device(gpu))
+    ref = torch.abs(ops.fft(seg[None, :])[0, :n // 2 + 1])
+    assert float(torch.max(torch.abs(mag - ref))) <= FFT_RTOL * float(torch.max(ref))
+    del seg, ref
+    xr[n // 2] = np.inf
+    mag = ops.spectrum(xr[None, :], 1000, n - 5000, n)[0]
+    assert not bool(torch.any(torch.isfinite(mag)))
+    del xr, mag
+    torch.cuda.empty_cache()
+    # 2^30, real input: cos tones, N/2 a_j at bins f_j and N - f_j
+    n = 1 << 30
+    fr, ar = [5, n // 3, n // 2 - 1], [0.5, -0.75, 0.25]
+    X = ops.fft(_tones(n, fr, ar, gpu, real=True)[None, :])[0]
+    want = torch.zeros(n, dtype=torch.complex64, device=gpu)
+    for fj, aj in zip(fr, ar):
+        want[fj] += n / 2 * aj
+        want[n - fj] += n / 2 * aj
+    err = float(torch.max(torch.abs(X - want)))
+    assert err <= FFT_RTOL * n / 2 * 0.75, err
+    del X, want
+    torch.cuda.empty_cache()
     with pytest.raises(RuntimeError):
-        _ops().fft(torch.zeros((1, 1 << 29), dtype=torch.complex64, device=gpu))
+        ops._log2(1 << 31)
 
 
 def test_spectrum_four_step_matches_reference(gpu):

@@ -1,0 +1,43 @@
+"""Times the four-step FFT paths on the device with HIP events; prints one
+line per size: ms per transform and the rate of its algorithmic traffic
+(read + write of N complex64 per pass: 2 passes for the two-step split, 3 for
+the three-pass one from 2^NEST, default 29; DSPCORE_LIB picks a build).
+    python tools/time_fft_nested.py [reps] [nest_from] [log2 sizes ...]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dsp-audio-project_amd"))
+from dspcore import ops  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    nest = int(sys.argv[2]) if len(sys.argv) > 2 else 29
+    sizes = [int(v) for v in sys.argv[3:]] or [22, 24, 26, 28, 29, 30]
+    dev = torch.device("cuda:0")
+    for lg in sizes:
+        n = 1 << lg
+        x = torch.randn(1, n, dtype=torch.complex64, device=dev)
+        out = torch.empty_like(x)
+        ops.fft(x, out)  # tables, workspace
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            ops.fft(x, out)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        passes = 3 if lg >= nest else 2
+        gbs = passes * 2 * n * 8 / (ms * 1e-3) / 1e9
+        print(f"2^{lg}: {ms:.3f} ms per transform, {passes} passes, {gbs:.0f} GB/s of "
+              f"read+write traffic", flush=True)
+        del x, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
