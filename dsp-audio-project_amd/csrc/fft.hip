@@ -1006,31 +1006,11 @@ int build_tw_coarse(const float2* tw, float2* twc, int log2n, hipStream_t s) {
   return DSP_OK;
 }
 
-// Step A's input: a non-finite value sets `nf` (the row's flag for the
-// non-finite repair, fft_nf.hip) and, for the complex transforms, reads as
+// Step A's input (f.hdr set): a non-finite value raises the row's flag for the
+// non-finite repair (fft_nf.hip) and, for the complex transforms, reads as
 // zero, so that the output holds the DFT of the finite part -- the values the
 // reference gives the components that no inf or NaN reaches.  (The spectrum's
 // bins all become +inf or NaN; the repair rewrites every one.)
-template <int MODE>
-__device__ __forceinline__ float2 load_input_nf(const FftArgs& a, const InRow& r, int n, bool& nf) {
-  if constexpr (MODE == kSpec) {
-    const float s = (n < r.valid) ? a.in[r.base + n] : 0.f;
-    nf |= !__builtin_isfinite(s);
-    return make_float2(s * a.win[n], 0.f);
-  } else {
-    float2 v = load_input<MODE>(a, r, n, true);
-    if (!__builtin_isfinite(v.x)) {
-      nf = true;
-      v.x = 0.f;
-    }
-    if (!__builtin_isfinite(v.y)) {
-      nf = true;
-      v.y = 0.f;
-    }
-    return v;
-  }
-}
-
 template <int LOG2A, int MODE>
 __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
   using PL = Plan<LOG2A>;
@@ -1047,13 +1027,41 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
   if ((gridDim.x & 7) == 0) gx = (gx & 7) * (gridDim.x >> 3) + (gx >> 3);
   const int64_t c0 = gx * KC;
   const InRow ir = in_row<MODE>(a, b);
-  bool nf = false;
-  for (int i = threadIdx.x; i < KC * NA; i += NT) {
-    const int c = i % KC, n2 = i / KC;
-    const int n = (int)(c0 + c + NB * n2);
-    lds[c * TS + lpad(n2)] = f.hdr ? load_input_nf<MODE>(a, ir, n, nf) : load_input<MODE>(a, ir, n, true);
+  // every load of the tile issued before the first use (PER per thread, in
+  // registers), then the non-finite scan, then LDS: a loop that stored each
+  // value as it arrived waited out one HBM round trip per value (round 5)
+  constexpr int PER = KC * NA / NT;
+  static_assert(PER * NT == KC * NA, "tile split");
+  float2 v[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = threadIdx.x + it * NT;
+    v[it] = load_input<MODE>(a, ir, (int)(c0 + i % KC + NB * (i / KC)), true);
   }
-  if (nf) f.hdr[2 * b] = 1u;
+  if (f.hdr) {
+    // (the spectrum only flags: s * w is non-finite exactly when the sample s
+    // is, w in [0, 1])
+    bool nf = false;
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      if (!__builtin_isfinite(v[it].x)) {
+        nf = true;
+        if constexpr (MODE != kSpec) v[it].x = 0.f;
+      }
+      if constexpr (MODE != kSpec) {
+        if (!__builtin_isfinite(v[it].y)) {
+          nf = true;
+          v[it].y = 0.f;
+        }
+      }
+    }
+    if (nf) f.hdr[2 * b] = 1u;
+  }
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = threadIdx.x + it * NT;
+    lds[(i % KC) * TS + lpad(i / KC)] = v[it];
+  }
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2A, 0> tw;
   load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA * f.tws);
@@ -1061,10 +1069,15 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
   run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
   __syncthreads();
   float2* y = f.ws + b * f.N;
-  for (int i = threadIdx.x; i < KC * NA; i += NT) {
+  // (unrolled by 4: the twiddle loads of 4 outputs in flight together, where
+  // the plain loop waited out one table round trip per output; fully
+  // unrolled the kernel took 148 VGPRs and spilled at 2^11)
+#pragma unroll 4
+  for (int it = 0; it < PER; ++it) {
+    const int i = threadIdx.x + it * NT;
     const int c = i % KC, k2 = i / KC;
-    const int64_t n1 = c0 + c;
-    y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], tw_step(f, n1 * k2 * f.tws));
+    y[(int64_t)k2 * NB + c0 + c] =
+        cmul(lds[c * TS + lpad(k2)], tw_step(f, (c0 + c) * (int64_t)k2 * f.tws));
   }
 }
 
@@ -1099,9 +1112,18 @@ __global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(
     out_k = NA;
   }
   const float2* y = f.ws + src0;
-  for (int i = threadIdx.x; i < KC * NB; i += NT) {
-    const int r = i / NB, n1 = i - r * NB;
-    lds[r * TS + lpad(n1)] = y[r * src_c + n1];
+  constexpr int PER = KC * NB / NT;
+  static_assert(PER * NT == KC * NB, "tile split");
+  float2 v[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {  // all loads in flight before the first LDS write
+    const int i = threadIdx.x + it * NT;
+    v[it] = y[(i / NB) * src_c + (i % NB)];
+  }
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = threadIdx.x + it * NT;
+    lds[(i / NB) * TS + lpad(i % NB)] = v[it];
   }
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2B, 0> tw;
