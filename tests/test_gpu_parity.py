@@ -898,7 +898,8 @@ def test_fft_nested_four_step(gpu):
     at 2^29 and a real row at 2^30; the 2^29 spectrum against |FFT| of the same
     windowed float32 row; an inf at n = 0 (every X[k].real +inf, X.imag the
     DFT of the rest) and in the spectrum's segment (every bin non-finite);
-    2^31 raises RuntimeError."""
+    the three-pass spectrum at 2^25 over three rows against numpy; 2^31
+    raises RuntimeError."""
     ops = _ops()
     n = 1 << 29
     f = [[3, 777777, n // 3, n - 5], [1, 2, n // 2, n - 1]]
@@ -936,6 +937,18 @@ def test_fft_nested_four_step(gpu):
     assert not bool(torch.any(torch.isfinite(mag)))
     del xr, mag
     torch.cuda.empty_cache()
+    # the three-pass spectrum from 2^25, three rows (row loop, segment offsets,
+    # zero padding) against numpy
+    n = 1 << 25
+    rng = np.random.default_rng(25)
+    xs = rng.uniform(-1, 1, (3, n + 3000)).astype(np.float32)
+    mag = ops.spectrum(torch.from_numpy(xs).to(gpu), 2000, n - 1000, n).cpu().numpy()
+    w = (0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n) / (n - 1))).astype(np.float32)
+    seg = np.zeros((3, n), dtype=np.float32)
+    seg[:, :n - 1000] = xs[:, 2000:n + 1000]
+    ref = np.abs(np.fft.rfft((seg * w).astype(np.float64), axis=1))
+    assert np.max(np.abs(mag - ref)) <= FFT_RTOL * np.max(ref)
+    del xs, mag, seg, ref
     # 2^30, real input: cos tones, N/2 a_j at bins f_j and N - f_j
     n = 1 << 30
     fr, ar = [5, n // 3, n // 2 - 1], [0.5, -0.75, 0.25]
