@@ -1011,10 +1011,9 @@ int build_tw_coarse(const float2* tw, float2* twc, int log2n, hipStream_t s) {
 // zero, so that the output holds the DFT of the finite part -- the values the
 // reference gives the components that no inf or NaN reaches.  (The spectrum's
 // bins all become +inf or NaN; the repair rewrites every one.)
-template <int LOG2A, int MODE>
-__global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
+template <int LOG2A, int MODE, int KC = kcols_for(LOG2A)>
+__global__ __launch_bounds__(KC * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
   using PL = Plan<LOG2A>;
-  constexpr int KC = kcols_for(LOG2A);
   constexpr int NA = PL::N, NT = KC * PL::TPT, TS = PL::PADN + 1;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const FftArgs& a = f.a;
@@ -1082,13 +1081,14 @@ __global__ __launch_bounds__(kcols_for(LOG2A) * Plan<LOG2A>::TPT) void k_fft4_a(
 }
 
 // Step B.  Nested (run_fft6_row, f.nest = the outer NA): the KC rows of a
-// workgroup are one inner row r = blockIdx.x of KC consecutive outer rows k2 =
-// blockIdx.y KC + c, so that the natural-order output k of (k2, r), X[k2 +
-// nest k], is written in runs of KC consecutive addresses.
-template <int LOG2B, int MODE>
-__global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
+// workgroup are one inner row r = blockIdx.y of KC consecutive outer rows k2 =
+// blockIdx.x KC + c, so that the natural-order output k of (k2, r), X[k2 +
+// nest k], is written in runs of KC consecutive addresses, and the workgroups
+// that write the other halves of those lines are dispatched to the same XCD
+// at the same time (blockIdx.x remapped as in step A).
+template <int LOG2B, int MODE, int KC = kcols_for(LOG2B)>
+__global__ __launch_bounds__(KC * Plan<LOG2B>::TPT) void k_fft4_b(Fft4Args f) {
   using PL = Plan<LOG2B>;
-  constexpr int KC = kcols_for(LOG2B);
   constexpr int NB = PL::N, NT = KC * PL::TPT, TS = PL::PADN + 1;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const FftArgs& a = f.a;
@@ -1097,7 +1097,9 @@ __global__ __launch_bounds__(kcols_for(LOG2B) * Plan<LOG2B>::TPT) void k_fft4_b(
   // out0 + c * out_c + k1 * out_k (complex / magnitude units)
   int64_t src0, src_c, out0, out_c, out_k;
   if (f.nest) {
-    const int64_t k2 = (int64_t)blockIdx.y * KC, r = blockIdx.x;
+    int64_t gx = blockIdx.x;
+    if ((gridDim.x & 7) == 0) gx = (gx & 7) * (gridDim.x >> 3) + (gx >> 3);
+    const int64_t k2 = gx * KC, r = blockIdx.y;
     src0 = k2 * f.N + r * NB;
     src_c = f.N;
     out0 = k2 + f.nest * r;
@@ -1187,26 +1189,25 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
   }
 }
 
-// Three-pass (nested) four-step from N = 2^DSP_FFT_NEST_FROM up to 2^30
-// (round 5; the reference's recursion has no size limit, dsp_core.py:41-66):
-// N = NA * NB with NB = NB1 * NB2 and all three at most 2^10 (so every
-// sub-transform moves 8 columns -- 64 B runs -- per HBM access; the two-step
+// Three-pass (nested) four-step from N = 2^25 up to 2^30 (round 5; the
+// reference's recursion has no size limit, dsp_core.py:41-66): N = NA * NB
+// with NB = NB1 * NB2, so that no sub-transform exceeds 2^11 points and every
+// HBM access is a run of 8 or 16 consecutive complex values (the two-step
 // split of 2^24 and up needs sub-transforms of 2^12..2^14, 4..1 columns):
 //   step A   (k_fft4_a<LA>): the NB columns of NA points of the row, the
 //            twiddle W_N^(n1 k2) on the way out -> Y[k2][n1] (rows of NB);
 //   step A'  (k_fft4_a<LA1>, complex): the NA rows' columns of NB1 points
 //            with W_NB = W_N^NA (table stride tws = NA) -> Y'[k2][..];
-//   step B'  (k_fft4_b<LB2>, nest = NA): rows of NB2 points, 8 outer rows k2
-//            per workgroup, natural-order output k of row k2 -> X[k2 + NA k].
-// One row at a time (the workspace is 2 N complex whatever B).
-// (From 2^25: the two-pass split's 2^12..2^14-point sub-transforms move 4..1
-// columns per access; round 5 measured 0.684 vs 0.715 ms at 2^25, 5.98 vs
-// 9.90 ms at 2^28, and the two-pass faster at 2^24, 0.290 vs 0.313 ms --
-// profiles/r05_fft_large.txt.)
-#ifndef DSP_FFT_NEST_FROM
-#define DSP_FFT_NEST_FROM 25
-#endif
-constexpr int kLog2Nested = DSP_FFT_NEST_FROM;
+//   step B'  (k_fft4_b<LB2>, nest = NA): rows of NB2 points, 8 or 16 outer
+//            rows k2 per workgroup, natural-order output k of row k2 ->
+//            X[k2 + NA k].
+// Steps A and B' touch HBM at megabyte strides, A' at kilobyte ones.  One row
+// at a time (the workspace is 2 N complex whatever B).  From 2^25: the
+// two-pass split's 2^12..2^14-point sub-transforms move 4..1 columns per
+// access; round 5 measured 0.684 vs 0.715 ms at 2^25, 5.98 vs 9.90 ms at 2^28
+// (first three-pass version), the two-pass faster at 2^24, 0.290 vs 0.313 ms
+// (profiles/r05_fft_large.txt).
+constexpr int kLog2Nested = 25;
 static_assert(kLog2Nested > DSP_MAX_LOG2N + 1 && kLog2Nested <= DSP_MAX_LOG2N_FFT, "nest from");
 
 template <int LA, int LA1, int LB2, int MODE>
@@ -1214,22 +1215,27 @@ int run_fft6_row(const FftArgs& row, float2* Y, float2* Y2, const float2* twc, u
                  hipStream_t s) {
   constexpr int64_t N = int64_t(1) << (LA + LA1 + LB2);
   constexpr int64_t NA = int64_t(1) << LA, NB = N / NA;
-  constexpr int KA = kcols_for(LA), K1 = kcols_for(LA1), KB = kcols_for(LB2);
-  static_assert(KA == kCols && K1 == kCols && KB == kCols && NA % KB == 0, "3-pass split");
+  // 16 columns (128-byte runs) for the two passes whose HBM side is strided
+  // by megabytes where the LDS image fits twice per CU (up to 2^9 points):
+  // tools/stride_probe.hip copies such columns at 4.4 TB/s in 128-byte runs,
+  // 2.9 in 64-byte runs; the middle pass (kilobyte strides, 5.0) keeps 8
+  constexpr int KA = LA <= 9 ? 16 : kCols, K1 = kcols_for(LA1);
+  constexpr int KB = LB2 <= 9 ? 16 : kCols;
+  static_assert(NA % KB == 0 && (NB >> LA1) % K1 == 0, "3-pass split");
   using PA = Plan<LA>;
   using P1 = Plan<LA1>;
   using PB = Plan<LB2>;
   const size_t sa = (size_t)KA * (PA::PADN + 1) * sizeof(float2);
   const size_t s1 = (size_t)K1 * (P1::PADN + 1) * sizeof(float2);
   const size_t sb = (size_t)KB * (PB::PADN + 1) * sizeof(float2);
-  if (int rc = allow_lds(k_fft4_a<LA, MODE>, sa)) return rc;
+  if (int rc = allow_lds(k_fft4_a<LA, MODE, KA>, sa)) return rc;
   if (int rc = allow_lds(k_fft4_a<LA1, kC2C>, s1)) return rc;
-  if (int rc = allow_lds(k_fft4_b<LB2, MODE>, sb)) return rc;
+  if (int rc = allow_lds(k_fft4_b<LB2, MODE, KB>, sb)) return rc;
   Fft4Args fa{row, Y, N, hdr};
   fa.twc = twc;
   fa.tsh = tw_shift(LA + LA1 + LB2);
-  hipLaunchKernelGGL((k_fft4_a<LA, MODE>), dim3((unsigned)(NB / KA), 1), dim3(KA * PA::TPT), sa, s,
-                     fa);
+  hipLaunchKernelGGL((k_fft4_a<LA, MODE, KA>), dim3((unsigned)(NB / KA), 1), dim3(KA * PA::TPT),
+                     sa, s, fa);
   DSP_LAUNCHED("k_fft4_a");
   // the inner transforms over the NA rows of Y: complex in, W_NB from the W_N
   // table at stride NA
@@ -1244,7 +1250,7 @@ int run_fft6_row(const FftArgs& row, float2* Y, float2* Y2, const float2* twc, u
   DSP_LAUNCHED("k_fft4_a");
   Fft4Args fb = f1;
   fb.nest = NA;
-  hipLaunchKernelGGL((k_fft4_b<LB2, MODE>), dim3((unsigned)(NB >> LB2), (unsigned)(NA / KB)),
+  hipLaunchKernelGGL((k_fft4_b<LB2, MODE, KB>), dim3((unsigned)(NA / KB), (unsigned)(NB >> LB2)),
                      dim3(KB * PB::TPT), sb, s, fb);
   DSP_LAUNCHED("k_fft4_b");
   return DSP_OK;
@@ -1259,12 +1265,16 @@ int dispatch6(const FftArgs& row, int log2n, float2* Y, float2* Y2, const float2
     case 22: return run_fft6_row<7, 7, 8, MODE>(row, Y, Y2, twc, hdr, s);
     case 23: return run_fft6_row<7, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
     case 24: return run_fft6_row<8, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
-    case 25: return run_fft6_row<8, 8, 9, MODE>(row, Y, Y2, twc, hdr, s);
-    case 26: return run_fft6_row<8, 9, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    // the strided passes (A, B') at most 2^9 where the split allows (16
+    // columns, 128-byte runs), the middle one takes the rest; round 5 measured
+    // 4.93 -> 4.46 ms at 2^28 against an even split with 8 columns, 2^30's
+    // 9 / 11 / 10 at 20.1 vs 20.7 ms for 10 / 10 / 10 (profiles/r05_fft_large.txt)
+    case 25: return run_fft6_row<8, 9, 8, MODE>(row, Y, Y2, twc, hdr, s);
+    case 26: return run_fft6_row<9, 8, 9, MODE>(row, Y, Y2, twc, hdr, s);
     case 27: return run_fft6_row<9, 9, 9, MODE>(row, Y, Y2, twc, hdr, s);
-    case 28: return run_fft6_row<9, 9, 10, MODE>(row, Y, Y2, twc, hdr, s);
-    case 29: return run_fft6_row<9, 10, 10, MODE>(row, Y, Y2, twc, hdr, s);
-    case 30: return run_fft6_row<10, 10, 10, MODE>(row, Y, Y2, twc, hdr, s);
+    case 28: return run_fft6_row<9, 10, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    case 29: return run_fft6_row<9, 11, 9, MODE>(row, Y, Y2, twc, hdr, s);
+    case 30: return run_fft6_row<9, 11, 10, MODE>(row, Y, Y2, twc, hdr, s);
     default: return set_error(DSP_EINVAL, "log2n=%d outside the three-pass range", log2n);
   }
 }
