@@ -323,8 +323,10 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
       v[b][r] = FIRST ? io.load(n) : buf[lpad(n)];
     }
   }
-  // every read of this pass precedes its (in-place) writes
-  if constexpr (!FIRST || IO::kLdsIn) __syncthreads();
+  // every read of this pass precedes its (in-place) writes (a barrier for LDS
+  // only: one that also drained global loads would wait out the four-step's
+  // twiddle loads that are meant to be in flight under the passes)
+  if constexpr (!FIRST || IO::kLdsIn) lds_barrier();
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int j = j0 + b * PL::TPT;
@@ -365,7 +367,7 @@ __device__ __forceinline__ void run_pass(const IO& io, float2* buf, int j0,
       else buf[lpad(k)] = v[b][r];
     }
   }
-  if constexpr (!LAST) __syncthreads();
+  if constexpr (!LAST) lds_barrier();
   if constexpr (P + 1 < PL::NP) {
     if constexpr (P == 0) run_pass<LOG2N, P + 1, IO, LOWREG>(io, buf, j0, tw);
     else run_pass<LOG2N, P + 1, IO, LOWREG>(io, buf, j0, tw.next);
@@ -985,6 +987,29 @@ __device__ __forceinline__ float2 tw_step(const Fft4Args& f, int64_t m) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// tw_step in two halves, so that the table loads can be issued long before
+// the value is needed (a select or product on the loaded values would make the
+// compiler wait for them at once): w = sgn * a * b.
+struct TwLoad {
+  float2 a, b;
+  float sgn;
+};
+__device__ __forceinline__ TwLoad tw_fetch(const Fft4Args& f, int64_t m) {
+  // branch-free (a branch would join the loaded values through copies, which
+  // wait for them): without the coarse table b is the table's W^0 = 1
+  const int64_t Nt = f.N * f.tws;
+  m &= Nt - 1;
+  const bool split = f.twc != nullptr, up = !split && m >= Nt / 2;
+  const float2* pa = split ? f.twc : f.a.tw;
+  const int64_t ia = split ? m >> f.tsh : (up ? m - Nt / 2 : m);
+  const int64_t ib = split ? m & ((int64_t(1) << f.tsh) - 1) : 0;
+  return TwLoad{pa[ia], f.a.tw[ib], up ? -1.f : 1.f};
+}
+__device__ __forceinline__ float2 tw_finish(const TwLoad& t) {
+  const float2 w = make_float2(t.a.x * t.b.x - t.a.y * t.b.y, t.a.x * t.b.y + t.a.y * t.b.x);
+  return make_float2(t.sgn * w.x, t.sgn * w.y);
+}
+
 __global__ __launch_bounds__(256) void k_tw_coarse(const float2* __restrict__ tw, float2* twc,
                                                    int64_t N, int tsh) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1064,19 +1089,35 @@ __global__ __launch_bounds__(KC * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
   const int tl = threadIdx.x / PL::TPT, j0 = threadIdx.x - tl * PL::TPT;
   Tw<LOG2A, 0> tw;
   load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA * f.tws);
-  __syncthreads();
+  // The inter-step twiddles W_Nt^(n1 k2) of this thread's outputs: its column
+  // n1 is fixed and k2 = r0 + it S, so exact table values at every 4th output
+  // and W^(n1 S j), j = 1..3, between (at most 3 roundings more than the
+  // table).  Their loads go out here, behind the passes' twiddles, so that
+  // they are in flight under the passes (the barriers below wait for LDS
+  // only); the epilogue loaded them itself, 4 outputs at a time -- 4 table
+  // round trips per tile, which held step A at ~2.1 TB/s against step B's 4.6.
+  constexpr int S = NT / KC;
+  static_assert(PER % 4 == 0 && NT % KC == 0, "twiddle anchors");
+  const int c = threadIdx.x % KC, r0 = threadIdx.x / KC;
+  const int64_t n1 = c0 + c;
+  TwLoad anc_l[PER / 4];
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) anc_l[q] = tw_fetch(f, n1 * (r0 + 4 * q * S) * f.tws);
+  const TwLoad s1_l = tw_fetch(f, n1 * S * f.tws);
+  lds_barrier();
   run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
-  __syncthreads();
+  lds_barrier();
+  float2 anc[PER / 4];
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) anc[q] = tw_finish(anc_l[q]);
+  const float2 s1 = tw_finish(s1_l), s2 = cmul(s1, s1), s3 = cmul(s2, s1);
   float2* y = f.ws + b * f.N;
-  // (unrolled by 4: the twiddle loads of 4 outputs in flight together, where
-  // the plain loop waited out one table round trip per output; fully
-  // unrolled the kernel took 148 VGPRs and spilled at 2^11)
-#pragma unroll 4
+#pragma unroll
   for (int it = 0; it < PER; ++it) {
-    const int i = threadIdx.x + it * NT;
-    const int c = i % KC, k2 = i / KC;
-    y[(int64_t)k2 * NB + c0 + c] =
-        cmul(lds[c * TS + lpad(k2)], tw_step(f, (c0 + c) * (int64_t)k2 * f.tws));
+    const int k2 = r0 + it * S;
+    const float2 w0 = anc[it / 4];
+    const float2 w = it % 4 == 0 ? w0 : cmul(w0, it % 4 == 1 ? s1 : it % 4 == 2 ? s2 : s3);
+    y[(int64_t)k2 * NB + n1] = cmul(lds[c * TS + lpad(k2)], w);
   }
 }
 
@@ -1178,18 +1219,12 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
     case 19: return launch_fft4<9, 10, MODE>(f, s);
     case 20: return launch_fft4<10, 10, MODE>(f, s);
     case 21: return launch_fft4<10, 11, MODE>(f, s);
-    case 22: return launch_fft4<11, 11, MODE>(f, s);
-    case 23: return launch_fft4<11, 12, MODE>(f, s);
-    case 24: return launch_fft4<12, 12, MODE>(f, s);
-    case 25: return launch_fft4<12, 13, MODE>(f, s);
-    case 26: return launch_fft4<13, 13, MODE>(f, s);
-    case 27: return launch_fft4<13, 14, MODE>(f, s);  // (one column per 2^14 workgroup:
-    case 28: return launch_fft4<14, 14, MODE>(f, s);  //  strided, not coalesced, loads)
+    case 22: return launch_fft4<11, 11, MODE>(f, s);  // (2^23 and up: run_fft6_row)
     default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
   }
 }
 
-// Three-pass (nested) four-step from N = 2^25 up to 2^30 (round 5; the
+// Three-pass (nested) four-step from N = 2^23 up to 2^30 (round 5; the
 // reference's recursion has no size limit, dsp_core.py:41-66): N = NA * NB
 // with NB = NB1 * NB2, so that no sub-transform exceeds 2^11 points and every
 // HBM access is a run of 8 or 16 consecutive complex values (the two-step
@@ -1202,12 +1237,12 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
 //            rows k2 per workgroup, natural-order output k of row k2 ->
 //            X[k2 + NA k].
 // Steps A and B' touch HBM at megabyte strides, A' at kilobyte ones.  One row
-// at a time (the workspace is 2 N complex whatever B).  From 2^25: the
+// at a time (the workspace is 2 N complex whatever B).  From 2^23: the
 // two-pass split's 2^12..2^14-point sub-transforms move 4..1 columns per
-// access; round 5 measured 0.684 vs 0.715 ms at 2^25, 5.98 vs 9.90 ms at 2^28
-// (first three-pass version), the two-pass faster at 2^24, 0.290 vs 0.313 ms
-// (profiles/r05_fft_large.txt).
-constexpr int kLog2Nested = 25;
+// access; with the twiddle loads under the passes (k_fft4_a) round 5 measured
+// 0.092 vs 0.111 ms at 2^23, 0.211 vs 0.274 at 2^24 and the two-pass faster at
+// 2^22, 0.052 vs 0.057 ms (profiles/r05_fft_large.txt).
+constexpr int kLog2Nested = 23;
 static_assert(kLog2Nested > DSP_MAX_LOG2N + 1 && kLog2Nested <= DSP_MAX_LOG2N_FFT, "nest from");
 
 template <int LA, int LA1, int LB2, int MODE>
@@ -1260,9 +1295,6 @@ template <int MODE>
 int dispatch6(const FftArgs& row, int log2n, float2* Y, float2* Y2, const float2* twc,
               uint32_t* hdr, hipStream_t s) {
   switch (log2n) {
-    case 20: return run_fft6_row<6, 7, 7, MODE>(row, Y, Y2, twc, hdr, s);
-    case 21: return run_fft6_row<7, 7, 7, MODE>(row, Y, Y2, twc, hdr, s);
-    case 22: return run_fft6_row<7, 7, 8, MODE>(row, Y, Y2, twc, hdr, s);
     case 23: return run_fft6_row<7, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
     case 24: return run_fft6_row<8, 8, 8, MODE>(row, Y, Y2, twc, hdr, s);
     // the strided passes (A, B') at most 2^9 where the split allows (16

@@ -202,7 +202,7 @@ def fft_diezmado_en_tiempo(x):
 
     Length <= 1 returns x unchanged (:52).  Power-of-two lengths up to 2^30
     give the natural-order DFT (complex128 for numpy input): one LDS-resident
-    launch up to 2^14, a four-step transform (two launches, three from 2^25)
+    launch up to 2^14, a four-step transform (two launches, three from 2^23)
     above.  Other lengths raise ValueError; powers of two above 2^30 raise
     RuntimeError.
     """

@@ -129,7 +129,7 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
  * Up to DSP_MAX_LOG2N one launch keeps each transform in LDS and needs no
  * workspace; above it a four-step transform keeps its intermediate in
  * `workspace` (device, 8-byte aligned, >= dsp_fft_workspace_bytes(B, log2n);
- * 0 below): up to 2^24 two launches over all rows, B * N * 8 bytes; from 2^25
+ * 0 below): up to 2^22 two launches over all rows, B * N * 8 bytes; from 2^23
  * (ABI 2.5, up to 2^30) three launches (a four-step nested in step B) row by
  * row, 2 * N * 8 bytes whatever B; plus, above 2^20, a coarse twiddle table of
  * 2^floor(log2n / 2) * 8 bytes, and a header of 8 bytes per row (per launch

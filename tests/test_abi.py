@@ -28,14 +28,15 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     assert rc == _lib.DSP_EINVAL and "L=0" in _lib.last_error()
     rc = lib.dsp_fft_c2c_f32(None, None, 1, 31, 1, 1 << 31, 1 << 31, None, None, 0, None)
     assert rc == _lib.DSP_EINVAL
-    # four-step sizes: the two-pass split (2^15..2^24) needs B * N complex, the
-    # three-pass one (2^25..2^30, row by row) 2 N complex; above 2^20 the
+    # four-step sizes: the two-pass split (2^15..2^22) needs B * N complex, the
+    # three-pass one (2^23..2^30, row by row) 2 N complex; above 2^20 the
     # coarse twiddle table, 2^floor(log2n / 2) complex; then the non-finite
     # header, 8 bytes per row (of a launch part of <= 65535 rows: two-pass)
     assert lib.dsp_fft_workspace_bytes(3, 14) == 0
     assert lib.dsp_fft_workspace_bytes(3, 15) == 3 * (1 << 15) * 8 + 3 * 8
     assert lib.dsp_fft_workspace_bytes(2, 22) == 2 * (1 << 22) * 8 + (1 << 11) * 8 + 2 * 8
-    assert lib.dsp_fft_workspace_bytes(3, 24) == 3 * (1 << 24) * 8 + (1 << 12) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 23) == 2 * (1 << 23) * 8 + (1 << 11) * 8 + 3 * 8
+    assert lib.dsp_fft_workspace_bytes(3, 24) == 2 * (1 << 24) * 8 + (1 << 12) * 8 + 3 * 8
     assert lib.dsp_fft_workspace_bytes(3, 25) == 2 * (1 << 25) * 8 + (1 << 12) * 8 + 3 * 8
     assert lib.dsp_fft_workspace_bytes(3, 26) == 2 * (1 << 26) * 8 + (1 << 13) * 8 + 3 * 8
     assert lib.dsp_fft_workspace_bytes(1, 28) == 2 * (1 << 28) * 8 + (1 << 14) * 8 + 8
