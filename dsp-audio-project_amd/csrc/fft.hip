@@ -1090,27 +1090,31 @@ __global__ __launch_bounds__(KC * Plan<LOG2A>::TPT) void k_fft4_a(Fft4Args f) {
   Tw<LOG2A, 0> tw;
   load_tw<LOG2A, 0>(tw, a.tw, j0, f.N / NA * f.tws);
   // The inter-step twiddles W_Nt^(n1 k2) of this thread's outputs: its column
-  // n1 is fixed and k2 = r0 + it S, so exact table values at every 4th output
-  // and W^(n1 S j), j = 1..3, between (at most 3 roundings more than the
-  // table).  Their loads go out here, behind the passes' twiddles, so that
+  // n1 is fixed and k2 = r0 + it S, so three table values -- W^(n1 r0),
+  // W^(n1 S), W^(4 n1 S) -- and products: W^(n1 (r0 + 4 q S)) by q - 1
+  // multiplications by W^(4 n1 S), then W^(n1 S j), j = 1..3 (at most 6
+  // roundings more than the table, ~4e-7; the passes' own twiddles chain up
+  // to 15).  Their loads go out here, behind the passes' twiddles, so that
   // they are in flight under the passes (the barriers below wait for LDS
-  // only); the epilogue loaded them itself, 4 outputs at a time -- 4 table
-  // round trips per tile, which held step A at ~2.1 TB/s against step B's 4.6.
+  // only).  Round 5: the epilogue loaded them itself, 4 outputs at a time --
+  // 4 table round trips per tile, which held step A at ~2.1 TB/s against step
+  // B's 4.6; fetched here as 4 anchors + W^(n1 S), 2^28 4.43 -> 3.55 ms; as
+  // these 3, 3.38 ms (fewer scattered table reads).
   constexpr int S = NT / KC;
   static_assert(PER % 4 == 0 && NT % KC == 0, "twiddle anchors");
   const int c = threadIdx.x % KC, r0 = threadIdx.x / KC;
   const int64_t n1 = c0 + c;
-  TwLoad anc_l[PER / 4];
-#pragma unroll
-  for (int q = 0; q < PER / 4; ++q) anc_l[q] = tw_fetch(f, n1 * (r0 + 4 * q * S) * f.tws);
+  const TwLoad a0_l = tw_fetch(f, n1 * r0 * f.tws);
+  const TwLoad s4_l = tw_fetch(f, n1 * 4 * S * f.tws);
   const TwLoad s1_l = tw_fetch(f, n1 * S * f.tws);
   lds_barrier();
   run_pass<LOG2A, 0>(LdsIO<NA>{lds + tl * TS}, lds + tl * TS, j0, tw);
   lds_barrier();
+  const float2 s1 = tw_finish(s1_l), s2 = cmul(s1, s1), s3 = cmul(s2, s1), s4 = tw_finish(s4_l);
   float2 anc[PER / 4];
+  anc[0] = tw_finish(a0_l);
 #pragma unroll
-  for (int q = 0; q < PER / 4; ++q) anc[q] = tw_finish(anc_l[q]);
-  const float2 s1 = tw_finish(s1_l), s2 = cmul(s1, s1), s3 = cmul(s2, s1);
+  for (int q = 1; q < PER / 4; ++q) anc[q] = cmul(anc[q - 1], s4);
   float2* y = f.ws + b * f.N;
 #pragma unroll
   for (int it = 0; it < PER; ++it) {
