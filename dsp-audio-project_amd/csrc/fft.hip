@@ -945,13 +945,15 @@ int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
 //   step B: X[k2 + NA k1] = sum_n1 Y[n1][k2] W_NB^(n1 k1)
 // Each workgroup runs KC sub-transforms of consecutive columns (step A) or
 // rows (step B) in LDS with the one-launch Stockham passes; the HBM side of
-// both steps moves KC consecutive complex values per index (8 -- 64 B -- for
-// sub-transforms up to 2^11; 4, 2, 1 for 2^12, 2^13, 2^14, whose LDS images
-// are larger: round 3 took the limit from 2^22 to 2^26, round 4 to 2^28), staged through LDS so
-// every global access is a run of consecutive addresses.  The
-// sub-transforms' twiddles come from the caller's W_N table at stride N/NA
-// (N/NB), the inter-step twiddle W_N^m from the same table (m < N/2, else its
-// negation).  The workspace holds Y: B x N complex.
+// both steps moves KC consecutive complex values per index (8 -- 64 B -- or
+// 16 for the three-pass split's megabyte-strided passes), staged through LDS
+// so that every global access is a run of consecutive addresses.  Up to 2^22
+// two launches (sub-transforms up to 2^11); from 2^23 step B is itself a
+// four-step (run_fft6_row).  The sub-transforms' twiddles come from the
+// caller's W_N table at stride N/NA (N/NB), the inter-step twiddle W_N^m from
+// the same table (m < N/2, else its negation), above 2^20 points as the
+// product of two factors from small contiguous tables (tw_fetch).  The
+// workspace holds Y: B x N complex (two launches) or Y, Y': 2 x N (three).
 // ---------------------------------------------------------------------------
 constexpr int kCols = 8;
 // Columns per workgroup for a sub-transform of 2^LOG2 points: KC images of
