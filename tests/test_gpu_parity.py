@@ -937,6 +937,17 @@ def test_fft_nested_four_step(gpu):
     assert not bool(torch.any(torch.isfinite(mag)))
     del xr, mag
     torch.cuda.empty_cache()
+    # the per-row non-finite flags of the three-pass path: an inf only in row 1
+    # of a 2^25 batch leaves row 0 bitwise the clean batch's
+    n = 1 << 25
+    xc = torch.randn(2, n, dtype=torch.complex64, device=gpu)
+    Xc = ops.fft(xc)
+    xc[1, 0] = complex(np.inf, 0.0)
+    Xi = ops.fft(xc)
+    assert torch.equal(Xi[0], Xc[0])
+    assert bool(torch.all(torch.isposinf(Xi[1].real)))
+    assert bool(torch.all(torch.isfinite(Xi[1].imag)))
+    del xc, Xc, Xi
     # the three-pass spectrum from 2^25, three rows (row loop, segment offsets,
     # zero padding) against numpy
     n = 1 << 25
