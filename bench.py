@@ -40,7 +40,8 @@ initialised), `config3` and `config5` (the other two batched configs on one
 GPU), `host_inclusive` (numpy in, H2D, chain, D2H of y/z/|X|, numpy out) and
 `copy_ceiling` and `mix_ceiling` (the HBM rate of streaming kernels with the
 chain kernel's 1 read : 2 writes mix, tools/ubench_rw_mix in a child
-process; roofline.frac_vs_mix_ceiling).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
+process; roofline.frac_vs_mix_ceiling) and `fft_2_28` (the three-pass FFT of
+one 2^28-point row: ms and its read+write rate; not part of the metric).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
 (tests of the rank launcher and sharding on CPU).
 """
 from __future__ import annotations
@@ -471,6 +472,40 @@ def copy_ceiling(device, nbytes=1 << 30, reps=20):
                    f"mean of {reps} after 3 warm, CUDA events"}
 
 
+def fft_large(device, log2n=28, reps=3):
+    """The three-pass four-step FFT of one complex row of 2^log2n points
+    (fft_diezmado_en_tiempo's size range above one workgroup's LDS): ms per
+    transform (HIP events, mean of `reps` after one warm call) and the rate of
+    its algorithmic traffic, read + write of N complex64 per pass.  Not part
+    of the chain metric; None if it fails."""
+    import torch
+    from dspcore import ops
+    try:
+        n = 1 << log2n
+        x = torch.randn(1, n, dtype=torch.complex64, device=device)
+        out = torch.empty_like(x)
+        ops.fft(x, out)
+        torch.cuda.synchronize(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            ops.fft(x, out)
+        e1.record()
+        torch.cuda.synchronize(device)
+        ms = e0.elapsed_time(e1) / reps
+        del x, out
+        torch.cuda.empty_cache()
+    except (RuntimeError, ValueError) as e:
+        return {"error": str(e)[:200]}
+    passes = 3
+    gbs = passes * 2 * n * 8 / (ms * 1e-3) / 1e9
+    return {"n": n, "ms": round(ms, 3), "passes": passes, "achieved_gbs": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "how": f"ops.fft of one complex64 row of 2^{log2n} (three launches of 8/16-column "
+                   f"LDS tiles + twiddle table gather), mean of {reps} after 1 warm, CUDA events "
+                   "around the calls (host overhead included)"}
+
+
 def mix_ceiling():
     """HBM ceiling for the chain kernel's traffic mix (1 read : 2 writes: x in,
     y and z out), measured by tools/ubench_rw_mix (streaming float4 kernels with
@@ -614,6 +649,7 @@ def main(argv=None):
         extras["host_inclusive"] = host_inclusive(device)
         extras["copy_ceiling"] = copy_ceiling(device)
         extras["mix_ceiling"] = mix_ceiling()
+        extras["fft_2_28"] = fft_large(device)
     ceiling = (extras.get("copy_ceiling") or {}).get("value")
     mix = (extras.get("mix_ceiling") or {}).get("value")
 
@@ -667,6 +703,7 @@ def main(argv=None):
             "host_inclusive": extras.get("host_inclusive"),
             "copy_ceiling": extras.get("copy_ceiling"),
             "mix_ceiling": extras.get("mix_ceiling"),
+            **({"fft_2_28": extras["fft_2_28"]} if extras.get("fft_2_28") else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
