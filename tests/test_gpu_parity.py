@@ -898,8 +898,9 @@ def test_fft_nested_four_step(gpu):
     at 2^29 and a real row at 2^30; the 2^29 spectrum against |FFT| of the same
     windowed float32 row; an inf at n = 0 (every X[k].real +inf, X.imag the
     DFT of the rest) and in the spectrum's segment (every bin non-finite);
-    the three-pass spectrum at 2^25 over three rows against numpy; 2^31
-    raises RuntimeError."""
+    the three-pass spectrum at 2^25 over three rows against numpy; Parseval
+    and linearity on dense random 2^27 input; per-row non-finite flags at
+    2^25; 2^31 raises RuntimeError."""
     ops = _ops()
     n = 1 << 29
     f = [[3, 777777, n // 3, n - 5], [1, 2, n // 2, n - 1]]
@@ -936,6 +937,21 @@ def test_fft_nested_four_step(gpu):
     mag = ops.spectrum(xr[None, :], 1000, n - 5000, n)[0]
     assert not bool(torch.any(torch.isfinite(mag)))
     del xr, mag
+    torch.cuda.empty_cache()
+    # dense random input through the three-pass path: Parseval (sum |X|^2 = N
+    # sum |x|^2, in float64 sums) and linearity, size-independent properties
+    n = 1 << 27
+    gen = torch.Generator(device=gpu).manual_seed(27)
+    xa = torch.randn(1, n, dtype=torch.complex64, device=gpu, generator=gen)
+    xb = torch.randn(1, n, dtype=torch.complex64, device=gpu, generator=gen)
+    Xa, Xb = ops.fft(xa), ops.fft(xb)
+    ex = float(torch.sum(torch.abs(xa.to(torch.complex128)) ** 2))
+    eX = float(torch.sum(torch.abs(Xa.to(torch.complex128)) ** 2))
+    assert abs(eX / (n * ex) - 1) < 1e-5, eX / (n * ex)
+    Xs = ops.fft(xa + 2 * xb)
+    lin = float(torch.max(torch.abs(Xs - (Xa + 2 * Xb))))
+    assert lin <= FFT_RTOL * float(torch.max(torch.abs(Xs))), lin
+    del xa, xb, Xa, Xb, Xs
     torch.cuda.empty_cache()
     # the per-row non-finite flags of the three-pass path: an inf only in row 1
     # of a 2^25 batch leaves row 0 bitwise the clean batch's
