@@ -1200,13 +1200,16 @@ int launch_fft4(const Fft4Args& f, hipStream_t s) {
   using PA = Plan<LOG2A>;
   using PB = Plan<LOG2B>;
   static_assert(LOG2A >= 4 && LOG2B >= LOG2A, "split");
-  constexpr int KA = kcols_for(LOG2A), KB = kcols_for(LOG2B);
+  // step A's columns 16 wide (128-byte runs) where two images fit a CU's LDS:
+  // batched 2^15 .. 2^18, 3.5-4.1 -> 4.1-4.3 TB/s (round 5,
+  // profiles/r05_fft_large.txt); step B reads whole rows either way
+  constexpr int KA = LOG2A <= 9 ? 16 : kcols_for(LOG2A), KB = kcols_for(LOG2B);
   const size_t sa = (size_t)KA * (PA::PADN + 1) * sizeof(float2);
   const size_t sb = (size_t)KB * (PB::PADN + 1) * sizeof(float2);
-  if (int rc = allow_lds(k_fft4_a<LOG2A, MODE>, sa)) return rc;
+  if (int rc = allow_lds(k_fft4_a<LOG2A, MODE, KA>, sa)) return rc;
   if (int rc = allow_lds(k_fft4_b<LOG2B, MODE>, sb)) return rc;
   const unsigned rows = (unsigned)f.a.B;
-  hipLaunchKernelGGL((k_fft4_a<LOG2A, MODE>), dim3((unsigned)(PB::N / KA), rows),
+  hipLaunchKernelGGL((k_fft4_a<LOG2A, MODE, KA>), dim3((unsigned)(PB::N / KA), rows),
                      dim3(KA * PA::TPT), sa, s, f);
   DSP_LAUNCHED("k_fft4_a");
   hipLaunchKernelGGL((k_fft4_b<LOG2B, MODE>), dim3((unsigned)(PA::N / KB), rows),

@@ -2,7 +2,8 @@
 line per size: ms per transform and the rate of its algorithmic traffic
 (read + write of N complex64 per pass: 2 passes for the two-step split, 3 for
 the three-pass one from 2^NEST, default 29; DSPCORE_LIB picks a build).
-    python tools/time_fft_nested.py [reps] [nest_from] [log2 sizes ...]"""
+    python tools/time_fft_nested.py [reps] [nest_from] [log2 sizes ...]
+FFT_ROWS_LOG2=k: 2^k / N rows per call (batched transforms) instead of one."""
 import os
 import sys
 
@@ -20,7 +21,8 @@ def main():
     dev = torch.device("cuda:0")
     for lg in sizes:
         n = 1 << lg
-        x = torch.randn(1, n, dtype=torch.complex64, device=dev)
+        rows = max(1, (1 << int(os.environ.get("FFT_ROWS_LOG2", "0"))) // n)
+        x = torch.randn(rows, n, dtype=torch.complex64, device=dev)
         out = torch.empty_like(x)
         ops.fft(x, out)  # tables, workspace
         torch.cuda.synchronize()
@@ -32,8 +34,8 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         passes = 3 if lg >= nest else 2
-        gbs = passes * 2 * n * 8 / (ms * 1e-3) / 1e9
-        print(f"2^{lg}: {ms:.3f} ms per transform, {passes} passes, {gbs:.0f} GB/s of "
+        gbs = passes * 2 * n * rows * 8 / (ms * 1e-3) / 1e9
+        print(f"2^{lg} x {rows}: {ms:.3f} ms per call, {passes} passes, {gbs:.0f} GB/s of "
               f"read+write traffic", flush=True)
         del x, out
         torch.cuda.empty_cache()
