@@ -980,18 +980,10 @@ struct Fft4Args {
 // workspace -- both contiguous and L2-resident, where the workgroup's W^(n1 k2)
 // alone are scattered over the whole table (one line fetched per 8-byte
 // twiddle: round 5 measured the 2^28 four-step at 0.49 TB/s).  One more
-// rounding (~1 ulp of 1), far inside the FFT's 1e-5.
-__device__ __forceinline__ float2 tw_step(const Fft4Args& f, int64_t m) {
-  const int64_t Nt = f.N * f.tws;
-  if (!f.twc) return tw_full(f.a.tw, m, Nt);
-  m &= Nt - 1;
-  const float2 a = f.twc[m >> f.tsh], b = f.a.tw[m & ((int64_t(1) << f.tsh) - 1)];
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-
-// tw_step in two halves, so that the table loads can be issued long before
-// the value is needed (a select or product on the loaded values would make the
-// compiler wait for them at once): w = sgn * a * b.
+// rounding (~1 ulp of 1), far inside the FFT's 1e-5.  In two halves, so that
+// the table loads can be issued long before the value is needed (a select or
+// product on the loaded values would make the compiler wait for them at
+// once): w = sgn * a * b.
 struct TwLoad {
   float2 a, b;
   float sgn;
@@ -1473,7 +1465,7 @@ constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
 // Two-pass sizes: [Y: B x N complex][coarse twiddles][non-finite header: 2
 // words per row of a launch part].  Three-pass (run_fft6_row, one row at a
 // time): [Y: N][Y': N complex][coarse twiddles][header: 2 words per row].
-// The coarse twiddle table (tw_step) above 2^20 points: 2^floor(log2n / 2)
+// The coarse twiddle table (tw_fetch) above 2^20 points: 2^floor(log2n / 2)
 // complex.
 size_t fft_workspace_bytes(int64_t B, int log2n) {
   if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
