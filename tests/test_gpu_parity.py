@@ -557,6 +557,31 @@ def test_chain_generic_single_pass(gpu, n_in, fs, L, M, K, B):
                  gpu).tile_len == 0
 
 
+def test_chain_two_launch_48k_to_44k1(gpu):
+    """48 kHz -> 44.1 kHz (L/M = 147/160, K = 1023): 147 phase classes of the
+    32-output sub-chunks are more than the single-pass kernels' LDS tables
+    hold, so the chain plans the two-launch path (SRC kernel, then the
+    cascade); its rows against the reference recipe (dsp_core.py:133-173,
+    216-254, 68-98), clip driven."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 3, 9600
+    cfg = ChainConfig(n_in, 48000, 147, 160, 1023, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 0
+    gen = torch.Generator(device=gpu).manual_seed(147)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[1] *= 40.0
+    y, z, mag = (t.cpu().numpy() for t in ch.run(x))
+    for b in range(B):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 147, 160, orc.CONFIG3_GAINS,
+                                       1023, 2048)
+        assert y.shape[1] == ry.size and z.shape[1] == rz.size
+        assert np.max(np.abs(y[b] - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - rmag)) <= CHAIN_MAG_RTOL * np.max(rmag)
+
+
 @pytest.mark.parametrize("B,n_in", [(1, 48000), (5, 48000), (9, 12000), (16, 4800)])
 def test_chain_config5_persistent_bitwise_chained(gpu, B, n_in):
     """Config 5's ratio (160/147, K = 1023) through the persistent single-pass
