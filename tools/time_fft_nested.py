@@ -33,7 +33,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
-        passes = 3 if lg >= nest else 2
+        passes = 1 if lg <= 14 else (3 if lg >= nest else 2)  # one LDS-resident launch to 2^14
         gbs = passes * 2 * n * rows * 8 / (ms * 1e-3) / 1e9
         print(f"2^{lg} x {rows}: {ms:.3f} ms per call, {passes} passes, {gbs:.0f} GB/s of "
               f"read+write traffic", flush=True)
