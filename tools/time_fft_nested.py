@@ -1,7 +1,7 @@
 """Times the four-step FFT paths on the device with HIP events; prints one
 line per size: ms per transform and the rate of its algorithmic traffic
 (read + write of N complex64 per pass: 2 passes for the two-step split, 3 for
-the three-pass one from 2^NEST, default 29; DSPCORE_LIB picks a build).
+the three-pass one from 2^NEST, default 23; DSPCORE_LIB picks a build).
     python tools/time_fft_nested.py [reps] [nest_from] [log2 sizes ...]
 FFT_ROWS_LOG2=k: 2^k / N rows per call (batched transforms) instead of one."""
 import os
@@ -16,7 +16,7 @@ from dspcore import ops  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    nest = int(sys.argv[2]) if len(sys.argv) > 2 else 29
+    nest = int(sys.argv[2]) if len(sys.argv) > 2 else 23
     sizes = [int(v) for v in sys.argv[3:]] or [22, 24, 26, 28, 29, 30]
     dev = torch.device("cuda:0")
     for lg in sizes:
