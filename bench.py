@@ -40,8 +40,11 @@ initialised), `config3` and `config5` (the other two batched configs on one
 GPU), `host_inclusive` (numpy in, H2D, chain, D2H of y/z/|X|, numpy out) and
 `copy_ceiling` and `mix_ceiling` (the HBM rate of streaming kernels with the
 chain kernel's 1 read : 2 writes mix, tools/ubench_rw_mix in a child
-process; roofline.frac_vs_mix_ceiling) and `fft_2_28` (the three-pass FFT of
-one 2^28-point row: ms and its read+write rate; not part of the metric).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
+process; roofline.frac_vs_mix_ceiling), `fft_2_28` (the three-pass FFT of
+one 2^28-point row: ms and its algorithmic rate; not part of the metric),
+`app_rerun` (one channel through the drop-in as app.py calls it, next to the
+oracle) and `ratio_sweep` (every L/M in 1..8 at 4096 channels: path taken
+and Msamples/s against the two-launch chain).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
 (tests of the rank launcher and sharding on CPU).
 """
 from __future__ import annotations
@@ -498,12 +501,144 @@ def fft_large(device, log2n=28, reps=3):
     except (RuntimeError, ValueError) as e:
         return {"error": str(e)[:200]}
     passes = 3
-    gbs = passes * 2 * n * 8 / (ms * 1e-3) / 1e9
-    return {"n": n, "ms": round(ms, 3), "passes": passes, "achieved_gbs": round(gbs, 1),
+    alg = 2 * n * 8                   # read N complex64, write N complex64
+    gbs = alg / (ms * 1e-3) / 1e9
+    moved = passes * 2 * n * 8        # what the three passes move (each reads and writes N)
+    return {"n": n, "ms": round(ms, 3), "passes": passes,
+            "algorithmic_bytes": alg, "achieved_gbs": round(gbs, 1),
             "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": moved, "traffic_gbs": round(moved / (ms * 1e-3) / 1e9, 1),
             "how": f"ops.fft of one complex64 row of 2^{log2n} (three launches of 8/16-column "
                    f"LDS tiles + twiddle table gather), mean of {reps} after 1 warm, CUDA events "
-                   "around the calls (host overhead included)"}
+                   "around the calls (host overhead included); frac = algorithmic bytes (one "
+                   "read + one write of the row) / time / 8 TB/s, traffic = the three passes' "
+                   "read + write"}
+
+
+def app_rerun(device, reps=5):
+    """The reference app's own call pattern: ONE
+    channel per Streamlit rerun through the drop-in module -- app.py:162-167
+    (conversion_tasa_muestreo then sistema_ecualizador) and the three spectra
+    of :203-205 (x, y and z, each on its first 100000 samples) -- on a
+    441000-sample channel (10 s at 44.1 kHz, the config-1 stand-in for the
+    missing FastCar.wav) with the config-3 gains, at L/M 2/1 and 3/2.  numpy in,
+    numpy out, as app.py calls it; ms per rerun (median of `reps` after one
+    warm) next to the oracle (oracle/dsp_ref_cpu.py, the reference's numpy /
+    scipy calls) on the same host and input, one process.  Not the metric."""
+    import numpy as np
+    import torch
+
+    from modules import dsp_core as dc
+    from oracle import dsp_ref_cpu as orc
+    fs, n, lim = 44100, 441000, 100000
+    t = np.arange(n) / fs
+    x = (0.6 * np.sin(2 * np.pi * 440.0 * t)
+         + 0.3 * np.random.default_rng(7).uniform(-1, 1, n)).astype(np.float32)
+    x /= np.max(np.abs(x))
+
+    def rerun_gpu(L, M):
+        y, fs2 = dc.conversion_tasa_muestreo(x, fs, M, L)
+        z = dc.sistema_ecualizador(y, fs2, CONFIG3_GAINS)
+        return (dc.calcular_espectro_magnitud(x[:lim], fs), dc.calcular_espectro_magnitud(y[:lim], fs2),
+                dc.calcular_espectro_magnitud(z[:lim], fs2))
+
+    def rerun_cpu(L, M):
+        y, fs2 = orc.resample(x, fs, M, L)
+        z = orc.equaliser(y, fs2, CONFIG3_GAINS)
+        return (orc.spectrum(x[:lim], fs), orc.spectrum(y[:lim], fs2), orc.spectrum(z[:lim], fs2))
+
+    def median_ms(fn, k):
+        fn()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(device)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return sorted(ts)[len(ts) // 2]
+
+    out = {}
+    with torch.cuda.device(device):
+        for L, M in ((2, 1), (3, 2)):
+            g = median_ms(lambda: rerun_gpu(L, M), reps)
+            c = median_ms(lambda: rerun_cpu(L, M), 3)
+            got, ref = rerun_gpu(L, M), rerun_cpu(L, M)
+            err = max(float(np.max(np.abs(a[1] - b[1]))) / float(np.max(b[1])) for a, b in zip(got, ref))
+            out[f"L{L}M{M}"] = {"gpu_ms_per_rerun": round(g, 3), "oracle_ms_per_rerun": round(c, 2),
+                                "speedup": round(c / g, 1), "max_rel_mag_err": float(f"{err:.3g}")}
+    out["how"] = ("modules/dsp_core.py drop-in, numpy in/out (H2D, kernels, D2H per call): "
+                  "conversion_tasa_muestreo + sistema_ecualizador (app.py:162-167) + three "
+                  "calcular_espectro_magnitud on the first 100000 samples of x, y, z "
+                  "(app.py:203-205), one 441000-sample channel (10 s @ 44.1 kHz, tone + noise "
+                  "stand-in for FastCar.wav), config-3 gains; median of 5 after 1 warm; oracle: "
+                  "the same calls through oracle/dsp_ref_cpu.py, 1 process, same host")
+    return out
+
+
+def ratio_sweep(device, channels=4096, steps=3):
+    """Every SRC ratio the app's sliders offer (L, M in 1..8, app.py:149-150)
+    at the default tap rule K = 40 max(L, M) + 1 (dsp_core.py:158), plus
+    config 1's 2/1 at K = 127, on `channels` x 48000 samples at 48 kHz with
+    the config-3 gains and the app's spectrum (2048 points of z[:100000],
+    app.py:202-205; 4096 points would hit the reference's non-power-of-two
+    segment ValueError at M/L = 6, 8): the path dsp_chain_f32 took
+    (single-pass kernel or the two-launch chain), Msamples/s of the default
+    path and of the two-launch chain (dsp_chain_path(1)) on the same input,
+    CUDA events around `steps` eager calls after one warm call."""
+    import torch
+
+    from dspcore import _lib
+    from dspcore.chain import Chain, ChainConfig
+    gen = torch.Generator(device=device).manual_seed(77)
+    x = torch.rand((channels, 48000), generator=gen, device=device) * 2 - 1
+
+    def timed(ch):
+        ch.run(x)
+        torch.cuda.synchronize(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            ch.run(x, check=False)
+        e1.record()
+        torch.cuda.synchronize(device)
+        ch.check()
+        return e0.elapsed_time(e1) / steps
+
+    rows = []
+    cases = [(L, M, None) for L in range(1, 9) for M in range(1, 9)] + [(2, 1, 127)]
+    for L, M, K in cases:
+        ch = Chain(ChainConfig(48000, 48000, L, M, K, CONFIG3_GAINS, n_fft=2048, limit_pts=100000),
+                   channels, device)
+        _lib.trace_enable(True)
+        _lib.trace_read()
+        ch.run(x)
+        names = sorted({nm for nm, _ in _lib.trace_read()})
+        _lib.trace_enable(False)
+        ms = timed(ch)
+        single = "chain_tile" in names
+        ms2 = None
+        if single:
+            prev = _lib.chain_path(1)
+            try:
+                ms2 = timed(ch)
+            finally:
+                _lib.chain_path(prev)
+        rate = lambda v: round(channels * 48000 / (v * 1e-3) / 1e6, 1)  # noqa: E731
+        rows.append({"L": L, "M": M, "K": ch.src.K, "path": "single-pass" if single else
+                     ("eq-only (SRC identity)" if ch.identity_src else "two-launch"),
+                     "tile_len": ch.tile_len, "ms": round(ms, 4), "msamples_s": rate(ms),
+                     **({"two_launch_ms": round(ms2, 4), "two_launch_msamples_s": rate(ms2),
+                         "speedup_vs_two_launch": round(ms2 / ms, 3)} if ms2 else {}),
+                     "kernels": names})
+        del ch
+        torch.cuda.empty_cache()
+    del x
+    torch.cuda.empty_cache()
+    sp = [r for r in rows if r["path"] == "single-pass"]
+    return {"channels": channels, "n_in": 48000, "fs": 48000, "steps": steps,
+            "single_pass_cases": len(sp), "cases": len(rows),
+            "min_speedup_vs_two_launch": min((r["speedup_vs_two_launch"] for r in sp), default=None),
+            "rows": rows}
 
 
 def mix_ceiling():
@@ -539,6 +674,8 @@ def main(argv=None):
     ap.add_argument("--no-extras", "--no-config3", dest="no_extras", action="store_true",
                     help="skip the config-3/config-5, host-inclusive and copy-ceiling "
                          "measurements at N = 1")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the L/M ratio sweep (every app ratio at 4096 channels)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every step from Python instead of replaying a HIP graph")
     args = ap.parse_args(argv)
@@ -647,10 +784,21 @@ def main(argv=None):
             del rx
             torch.cuda.empty_cache()
         extras["host_inclusive"] = host_inclusive(device)
+        extras["app_rerun"] = app_rerun(device)
+        if not args.no_sweep:
+            extras["ratio_sweep"] = ratio_sweep(device)
         extras["copy_ceiling"] = copy_ceiling(device)
         extras["mix_ceiling"] = mix_ceiling()
         extras["fft_2_28"] = fft_large(device)
+    # the copy ceiling is the higher of torch's copy_ and the nt float4 1R:1W
+    # stream of tools/ubench_rw_mix (torch's alone flattered)
+    ceiling_src = None
     ceiling = (extras.get("copy_ceiling") or {}).get("value")
+    if ceiling:
+        ceiling_src = "torch copy_"
+    nt_copy = (extras.get("mix_ceiling") or {}).get("copy_1r1w_gbs")
+    if nt_copy and (not ceiling or nt_copy > ceiling):
+        ceiling, ceiling_src = nt_copy, "tools/ubench_rw_mix nt float4 1R:1W"
     mix = (extras.get("mix_ceiling") or {}).get("value")
 
     if rank == 0:
@@ -684,6 +832,7 @@ def main(argv=None):
                                 if traffic else None),
                 "traffic_source": traffic_src if traffic else None,
                 "copy_ceiling_gbs": ceiling,
+                "copy_ceiling_source": ceiling_src,
                 "frac_vs_copy_ceiling": round(achieved / ceiling, 4) if ceiling else None,
                 "mix_ceiling_gbs": mix,
                 "frac_vs_mix_ceiling": round(achieved / mix, 4) if mix else None,
@@ -701,6 +850,8 @@ def main(argv=None):
             **({"per_rank": per_rank} if per_rank else {}),
             **{k: extras.get(k) for k in ("config3", "config4", "config5") if k in extras},
             "host_inclusive": extras.get("host_inclusive"),
+            "app_rerun": extras.get("app_rerun"),
+            **({"ratio_sweep": extras["ratio_sweep"]} if extras.get("ratio_sweep") else {}),
             "copy_ceiling": extras.get("copy_ceiling"),
             "mix_ceiling": extras.get("mix_ceiling"),
             **({"fft_2_28": extras["fft_2_28"]} if extras.get("fft_2_28") else {}),

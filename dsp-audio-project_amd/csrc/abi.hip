@@ -80,7 +80,9 @@ int dsp_version(void) {
   // reference's labels (fft_nf.hip); dsp_fft_workspace_bytes adds the
   // four-step's per-row header; dsp_lfilter_nonfinite_f32 (round 5).
   // 2.5.0: DSP_MAX_LOG2N_FFT 28 -> 30 (nested four-step, round 5).
-  return 20500;
+  // 2.6.0: dsp_lfilter_nonfinite_f32 scans x for a / a0 = [1, 0, ...];
+  // single-pass chain kernels for every app ratio (round 6).
+  return 20600;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }

@@ -18,13 +18,21 @@
 //
 // k_lfilter_nf restores lfilter's labels after the cascade: one wave per row
 // reads y[n-1] (the cascade leaves it non-finite exactly when x held an inf or
-// NaN) and exits when it is finite; a flagged row finds k0, then runs the
+// NaN) and exits when it is finite -- except when a / a0 = [1, 0, ...], whose
+// finite values the caller computed as a convolution (design.py 'fir_rec':
+// y[n-1] is finite again len(b) samples after an inf), where every row scans
+// x; a flagged row finds k0, then runs the
 // recursion above on CLASSES -- finite values as 0, +-inf, NaN; coefficients
 // as their signs +-1 or 0 -- which is lfilter's own inf / NaN arithmetic (the
 // class of a sum or product does not depend on finite magnitudes), with the
 // state in LDS and the lanes updating it in parallel, and writes y[k] for k >=
 // k0.  Once every state is NaN, every later y is NaN and the wave fills the
-// rest of the row.
+// rest of the row.  The class state of a stretch of finite x evolves on its
+// own; when a whole chunk of finite x leaves it where the chunk started, the
+// labels repeat with the chunk (period | 64), and later chunks of finite x are
+// filled from the previous one without running the recursion (a one-pole
+// low-pass keeps +inf forever, a negative pole alternates its sign: without
+// this, millions of samples ran one by one).
 #include "common.h"
 
 namespace dsp {
@@ -37,6 +45,7 @@ struct LfNfArgs {
   float* y;
   int64_t B, n, ld_x, ld_y;
   int D;  // recursion order: max(len(a), len(b)) - 1, 1..DSP_LFILTER_NF_MAX
+  int scan_x;  // a / a0 = [1, 0, ...]: y[n-1] says nothing, scan every row's x
   // signs of b / a0 and a / a0, 2 bits each (0: zero, 1: +, 2: -), 16 a word
   uint32_t b[kLfWords], a[kLfWords];
 };
@@ -50,6 +59,10 @@ __device__ __forceinline__ float lf_cls(float v) {
   return __builtin_isfinite(v) ? 0.f : v;  // +-inf and NaN are their own class
 }
 
+__device__ __forceinline__ bool lf_same(float u, float v) {
+  return u == v || (u != u && v != v);  // classes: 0, +-inf, NaN
+}
+
 // Orders this wave's LDS accesses (they execute in order within a wave; this
 // keeps the compiler from moving them across the state update).
 __device__ __forceinline__ void lf_order() {
@@ -59,13 +72,13 @@ __device__ __forceinline__ void lf_order() {
 }
 
 __global__ __launch_bounds__(kWave) void k_lfilter_nf(LfNfArgs p) {
-  extern __shared__ float zs[];  // two state buffers of D
+  extern __shared__ float zs[];  // three state buffers of D: current, next, chunk start
   const int64_t r = blockIdx.x;
   const int lane = threadIdx.x;
   const int D = p.D;
   const float* x = p.x + r * p.ld_x;
   float* y = p.y + r * p.ld_y;
-  if (__builtin_isfinite(y[p.n - 1])) return;
+  if (!p.scan_x && __builtin_isfinite(y[p.n - 1])) return;
   // k0: the first non-finite input
   int64_t k0 = -1;
   for (int64_t base = 0; base < p.n && k0 < 0; base += kWave) {
@@ -79,12 +92,23 @@ __global__ __launch_bounds__(kWave) void k_lfilter_nf(LfNfArgs p) {
   const float b0 = lf_sign(p.b, 0);
   float* cur = zs;
   float* nxt = zs + D;
+  float* start = zs + 2 * D;
   int64_t c = k0 - (k0 % kWave);  // chunk of kWave samples: lane j holds x[c + j], y[c + j]
   bool saturated = false;
+  bool periodic = false;  // the last chunk's labels repeat while x stays finite
+  float yprev = 0.f;
 #pragma unroll 1
   for (; c < p.n && !saturated; c += kWave) {
     const int64_t kl = c + lane;
     const float xv = kl < p.n ? x[kl] : 0.f;
+    const bool fin = __ballot(!__builtin_isfinite(xv)) == 0;
+    if (periodic && fin) {
+      if (kl < p.n) y[kl] = yprev;  // (the state is unchanged)
+      continue;
+    }
+    periodic = false;
+    lf_order();
+    for (int i = lane; i < D; i += kWave) start[i] = cur[i];
     float ymine = 0.f;
     const int j0 = c < k0 ? (int)(k0 - c) : 0;
     const int j1 = p.n - c < kWave ? (int)(p.n - c) : kWave;
@@ -105,9 +129,16 @@ __global__ __launch_bounds__(kWave) void k_lfilter_nf(LfNfArgs p) {
     if (kl >= k0 && kl < c + j1) y[kl] = ymine;
     // every state NaN: every later y is NaN
     lf_order();
-    bool nan = true;
-    for (int i = lane; i < D; i += kWave) nan &= cur[i] != cur[i];
+    bool nan = true, same = true;
+    for (int i = lane; i < D; i += kWave) {
+      nan &= cur[i] != cur[i];
+      same &= lf_same(cur[i], start[i]);
+    }
     saturated = __ballot(!nan) == 0;
+    // a whole chunk of finite x that returned the state to its start: the
+    // labels are periodic with a period dividing kWave
+    periodic = fin && j0 == 0 && j1 == kWave && __ballot(!same) == 0;
+    yprev = ymine;
   }
   for (int64_t j = c + lane; j < p.n; j += kWave) y[j] = __builtin_nanf("");
 }
@@ -125,7 +156,9 @@ int launch_lfilter_nf(const float* x, float* y, int64_t B, int64_t n, int64_t ld
   DSP_REQUIRE(a[0] != 0.0, "a[0] == 0");
   if (B == 0 || n == 0) return DSP_OK;
   DSP_REQUIRE(x && y, "null pointer");
-  LfNfArgs p{x, y, B, n, ld_x, ld_y, D, {}, {}};
+  bool fir = true;  // a / a0 = [1, 0, ...]: the caller convolved (design.py 'fir_rec')
+  for (int i = 1; i < na; ++i) fir &= a[i] == 0.0;
+  LfNfArgs p{x, y, B, n, ld_x, ld_y, D, fir ? 1 : 0, {}, {}};
   auto put = [&](uint32_t* w, int i, const double* c, int nc) {
     const double q = i < nc ? c[i] / a[0] : 0.0;  // lfilter pads the shorter one with zeros
     w[i >> 4] |= (q > 0 ? 1u : (q < 0 ? 2u : 0u)) << (2 * (i & 15));
@@ -139,7 +172,7 @@ int launch_lfilter_nf(const float* x, float* y, int64_t B, int64_t n, int64_t ld
     q.B = B - b0 < (1 << 30) ? B - b0 : (1 << 30);
     q.x = x + b0 * ld_x;
     q.y = y + b0 * ld_y;
-    hipLaunchKernelGGL(k_lfilter_nf, dim3((unsigned)q.B), dim3(kWave), 2 * (size_t)D * sizeof(float),
+    hipLaunchKernelGGL(k_lfilter_nf, dim3((unsigned)q.B), dim3(kWave), 3 * (size_t)D * sizeof(float),
                        s, q);
     DSP_LAUNCHED("k_lfilter_nf");
   }

@@ -198,7 +198,9 @@ class LfilterPlan:
     x)[:n] (a gain when b has length 1), as a causal convolution on the SRC
     kernel with L = M = 1.  That keeps lfilter's non-finite semantics of the
     case: an inf or NaN meets every tap of b, a zero tap included (0 * inf =
-    NaN), and stays within len(b) samples."""
+    NaN), and stays within len(b) samples; 'fir_rec' -- a = [1, 0, ...] with
+    more than 3 coefficients: the same convolution for the finite values, then
+    lfilter's recursion labels (b, a kept for dsp_lfilter_nonfinite_f32)."""
     kind: str
     sos: np.ndarray | None = None
     taps: np.ndarray | None = None
@@ -233,6 +235,14 @@ def lfilter_plan(b, a) -> LfilterPlan:
     a_tail = np.trim_zeros(a[1:], "b")
     if max(a.size, b.size) <= 3:
         return LfilterPlan("sos", sos=tf_to_sos_row(b, a).reshape(1, 5), b=b, a=a)
+    if a_tail.size == 0:
+        # a = [1, 0, ...]: the transfer function is the FIR b, but lfilter runs
+        # its recursion (0 * inf = NaN labels everything after an inf).  The
+        # finite values are the convolution (tf2sos of a long b would factor a
+        # degree len(b) - 1 polynomial: 0.33 error at 101 taps, 5e30 at 301);
+        # the labels come from dsp_lfilter_nonfinite_f32, which scans x for
+        # this a (include/dspcore.h).
+        return LfilterPlan("fir_rec", taps=b.copy(), b=b, a=a)
     import scipy.signal
     sos6 = scipy.signal.tf2sos(b, np.concatenate([[1.0], a_tail]))  # rows b0 b1 b2 1 a1 a2
     sos = np.ascontiguousarray(np.column_stack([sos6[:, 0:3] / sos6[:, 3:4],

@@ -288,21 +288,32 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
     stays within len(b) samples as in lfilter; otherwise, after the cascade,
     one launch gives every output from the first inf or NaN on the +inf / -inf
     / NaN that lfilter's recursion gives it (dsp_lfilter_nonfinite_f32; orders
-    up to 4096).  a[0] == 0 raises ValueError as lfilter does.
+    up to 4096; above that the relabelling is skipped and a row keeps the
+    cascade's all-NaN after its first non-finite sample).  a = [1, 0, ...] with
+    a long b (an FIR through lfilter's recursion) convolves like the len(a) == 1
+    case and then takes the recursion's labels.  a[0] == 0 raises ValueError as
+    lfilter does.
     """
     plan = _design.lfilter_plan(b, a)
     ops = _ops()
+    from dspcore import _lib
+    # lfilter's recursion order (D = max(len(a), len(b)) - 1); above
+    # DSP_LFILTER_NF_MAX the inf / NaN relabelling is not run: such rows keep
+    # the cascade's all-NaN after the first non-finite sample (finite input is
+    # unaffected).
+    relabel = plan.kind != "fir" and max(plan.a.size, plan.b.size) - 1 <= _lib.DSP_LFILTER_NF_MAX
 
     def run(t, B):
-        if plan.kind == "fir":
+        x0 = t
+        if plan.kind in ("fir", "fir_rec"):
             n = int(t.shape[1])
             src = _design.SrcPlan(1, 1, int(plan.taps.size), plan.taps, 0, n, n, 0)
-            return ops.src_polyphase(t, src)
-        x0 = t
-        for group in _design.lfilter_groups(plan.sos):   # any order: <= 16 sections a launch
-            t = _cascade(ops, t, group, False, B)
+            t = ops.src_polyphase(t, src)
+        else:
+            for group in _design.lfilter_groups(plan.sos):   # any order: <= 16 sections a launch
+                t = _cascade(ops, t, group, False, B)
         # inf / NaN from x's first non-finite sample on as lfilter labels them
-        return ops.lfilter_nonfinite(x0, t, plan.b, plan.a)
+        return ops.lfilter_nonfinite(x0, t, plan.b, plan.a) if relabel else t
     return _run(x_n, run, np.float64)
 
 

@@ -107,7 +107,13 @@ int dsp_biquad_cascade_f32(const float* x, float* y, int64_t B, int64_t n,
  * the first inf or NaN of x on the class -- +inf, -inf or NaN -- that its
  * float64 arithmetic gives (a one-pole low-pass keeps +inf, a section with b1
  * == a1 makes NaN), while the cascade makes them all NaN.  Rows whose y[n-1]
- * is finite (no non-finite input) are left as they are, after one read.
+ * is finite (no non-finite input) are left as they are, after one read --
+ * except when a / a0 = [1, 0, ...] (an FIR through lfilter's recursion, whose
+ * finite values the caller computes as a convolution on dsp_src_polyphase_f32:
+ * y[n-1] is finite again len(b) samples after an inf), where every row's x is
+ * scanned.  Long stretches of finite x after the first inf or NaN whose class
+ * state repeats (a pole that keeps +inf, or alternates its sign) are filled
+ * without running the recursion sample by sample.
  * b (nb >= 1) and a (na >= 2, a[0] != 0) are HOST float64 arrays; D =
  * max(na, nb) - 1 <= DSP_LFILTER_NF_MAX.  x and y are [B][ld] float32 device
  * rows and must not alias.  (len(a) == 1 is lfilter's convolution: run it on
@@ -133,7 +139,10 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
  * (ABI 2.5, up to 2^30) three launches (a four-step nested in step B) row by
  * row, 2 * N * 8 bytes whatever B; plus, above 2^20, a coarse twiddle table of
  * 2^floor(log2n / 2) * 8 bytes, and a header of 8 bytes per row (per launch
- * part of at most 65535 rows for two launches).
+ * part of at most 65535 rows for two launches).  Size the workspace with
+ * dsp_fft_workspace_bytes, never with a formula of your own: the size grew in
+ * ABI 2.4 (per-row header) and 2.5 (coarse table, three-pass rows), and a
+ * smaller buffer is refused with DSP_EINVAL.
  * Non-finite input (ABI 2.4): every output component gets the class --
  * finite, +inf, -inf or NaN -- that the reference's recursive radix-2 DIT in
  * complex128 numpy arithmetic gives it (inf * 0 = NaN at the k = 0 twiddles,

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20500     # 2.5.0: FFT to 2^30 (2.4.0: FFT/spectrum non-finite repair)
+    assert lib.dsp_version() == 20600     # 2.6.0: lfilter relabel scan mode, single-pass ratios (2.5.0: FFT to 2^30)
     assert isinstance(_lib.last_error(), str)
 
 

@@ -32,6 +32,7 @@ and outside it: every output component's class is the oracle's (NaN / +inf /
 tolerance.
 """
 import contextlib
+import time
 import warnings
 
 import numpy as np
@@ -421,6 +422,10 @@ LFILTER_CASES = [
     ("trailing zeros of a count", [1.0], [1.0, -0.5, 0.0, 0.0]),
     ("b longer than a", [0.2, 0.3, -0.1, 0.05, 0.4, 0.1], [1.0, -0.5, 0.2]),
     ("butter 4 (four sections' worth of order)", "butter", None),
+    # a = [1, 0, ...] with a long b: convolved, then the recursion's labels
+    # (dsp_lfilter_nonfinite_f32 scans x: y[n-1] is finite again after len(b))
+    ("fir 101 through the recursion (a = [1, 0])", "firwin101", None),
+    ("fir 301 through the recursion (a = [2, 0, 0])", "firwin301", None),
 ]
 
 
@@ -431,6 +436,10 @@ def _lfilter_coeffs(b, a):
         return design.peaking_biquad(1000.0, 48000.0, 6.0)
     if b == "butter":
         return ss.butter(4, 0.2)
+    if b == "firwin101":
+        return ss.firwin(101, 0.2), np.array([1.0, 0.0])
+    if b == "firwin301":
+        return ss.firwin(301, 0.1), np.array([2.0, 0.0, 0.0])
     return np.asarray(b, dtype=np.float64), np.asarray(a, dtype=np.float64)
 
 
@@ -463,3 +472,35 @@ def test_nonfinite_lfilter_matches_scipy(gpu, name, b, a):
         scale = max(1.0, float(np.max(np.abs(want[r][fin]))) if fin.any() else 1.0)
         _same(y[r], want[r], EQ_ATOL * scale, f"{name} row {r} {specs[r]}")
     _same(y1, want[3], EQ_ATOL * 10, f"{name} 1-D")
+
+
+@pytest.mark.parametrize("name,b,a", [("one-pole low-pass", [0.5, 0.5], [1.0, -0.3]),
+                                      ("negative pole", [1.0], [1.0, 0.6]),
+                                      ("fir 101, a = [1, 0]", "firwin101", None)],
+                         ids=["lowpass", "negpole", "fir101"])
+def test_nonfinite_lfilter_long_rows(gpu, name, b, a):
+    """Rows of 2^21 samples whose labels never turn all-NaN (+inf kept by a
+    one-pole low-pass, a sign alternating with a negative pole) and a second
+    inf of the other sign 1.5 M samples later (NaN from there): the relabel
+    kernel fills the periodic stretches without running the class recursion
+    sample by sample (seconds per row before), and y's masks
+    are scipy.signal.lfilter's exactly."""
+    import scipy.signal as ss
+    from modules import dsp_core as dc
+    b, a = _lfilter_coeffs(b, a)
+    n = 1 << 21
+    x = np.random.default_rng(9).uniform(-1, 1, (3, n)).astype(np.float32)
+    x[0, 5] = INF
+    x[1, 70] = -INF
+    x[2, 64] = INF
+    x[2, 1_500_000] = -INF
+    with _quiet():
+        want = [ss.lfilter(b, a, row.astype(np.float64)) for row in x]
+        t0 = time.perf_counter()
+        y = dc.aplicar_ecuacion_diferencias(x, b, a)
+        wall = time.perf_counter() - t0
+    for r in range(x.shape[0]):
+        fin = np.isfinite(want[r])
+        scale = max(1.0, float(np.max(np.abs(want[r][fin]))) if fin.any() else 1.0)
+        _same(y[r], want[r], EQ_ATOL * scale, f"{name} row {r}")
+    assert wall < 5.0, wall

@@ -231,6 +231,10 @@ def _lfilter_cases():
         ("fir 2, a = [2]", [0.5, -0.5], [2.0]),
         ("fir 5 through the recursion (a = [1, 0])", [1.0, 2.0, 3.0, 4.0, 5.0], [1.0, 0.0]),
         ("gain through the recursion (a = [2, 0])", [3.0], [2.0, 0.0]),
+        # long FIRs through the recursion: convolved, not factored (tf2sos of a
+        # degree-300 polynomial is off by 5e30)
+        ("fir 101 through the recursion (a = [1, 0])", ss.firwin(101, 0.2), [1.0, 0.0]),
+        ("fir 301 through the recursion (a = [2, 0, 0])", ss.firwin(301, 0.1), [2.0, 0.0, 0.0]),
     ]
 
 
@@ -250,7 +254,8 @@ def test_lfilter_plan_any_order_matches_lfilter():
             got = ss.sosfilt(sos6, x)
             assert plan.sos.shape[0] <= design.MAX_LFILTER_SECTIONS
         else:
-            assert plan.kind == "fir" and np.size(a) == 1
+            assert (plan.kind == "fir" and np.size(a) == 1) or (
+                plan.kind == "fir_rec" and not np.any(np.asarray(a)[1:]))
             got = np.convolve(x, plan.taps)[:x.size]
         assert np.max(np.abs(got - ref)) <= 1e-9 * max(1.0, np.max(np.abs(ref))), name
     with pytest.raises(ValueError, match="a\\[0\\] == 0"):
