@@ -1,0 +1,3 @@
+// Per-phase single-pass chain kernels, unit 1 of 4 (chain_pp.h, chain_pp_unit.inc).
+#define PP_UNIT 1
+#include "chain_pp_unit.inc"

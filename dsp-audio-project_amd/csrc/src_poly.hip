@@ -100,7 +100,8 @@ __device__ __forceinline__ void store_tile(float* __restrict__ yr,
 // window start) against taps (h[2p - a], h[2p + 1 - a]), h[u] = P[phi][T-1-u]
 // (0 outside [0, T)); y = even + odd.  This is the canonical summation order
 // of the SRC for even M; the single-pass chain kernel (chain_tile.hip) uses
-// it too, so both produce bitwise the same y.  Odd M sums the taps in order.
+// it too, so both produce bitwise the same y.  Odd M sums even and odd u in
+// two chains (the same partial sums: y = chain 0 + chain 1).
 // ---------------------------------------------------------------------------
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -172,19 +173,25 @@ __global__ __launch_bounds__(NT) void k_src_reg(
 #pragma unroll
       for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r].x + acc[r].y;
     } else {
+      // odd M: two chains, over even and odd u (round 6: the canonical order,
+      // as k_src_generic and the per-phase single-pass kernels sum, so y is
+      // bitwise theirs; one chain before)
       const float* w = s_win + (int)(q - (T - 1) - qa);
       const float* h = s_bank + phi * TP;
-      float acc[R];
+      float acc[R], acc1[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.f;
+      for (int r = 0; r < R; ++r) acc[r] = acc1[r] = 0.f;
 #pragma unroll
       for (int u = 0; u < T; ++u) {
         const float t = h[u];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = fmaf(t, w[r * M + u], acc[r]);
+        for (int r = 0; r < R; ++r) {
+          if (u & 1) acc1[r] = fmaf(t, w[r * M + u], acc1[r]);
+          else acc[r] = fmaf(t, w[r * M + u], acc[r]);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r];
+      for (int r = 0; r < R; ++r) s_out[lbase + r * L] = acc[r] + acc1[r];
     }
   }
   __syncthreads();
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(NT) void k_src_reg(
       const int64_t j = (m0 + i) * M + c, q = j / L;
       const int base = (int)(q - qa);
       float nfs, fin, v = s_out[i];
-      window_sums(taps, K, L, (int)(j - q * L), thr, PACK ? (int)(q & 1) : -1,
+      window_sums(taps, K, L, (int)(j - q * L), thr, PACK ? (int)(q & 1) : T - 1,
                   [&](int t) { return s_win[base - t]; }, nfs, fin);
       nf_fix(v, nfs, fin);
       s_out[i] = v;

@@ -165,7 +165,10 @@ def test_chain_path_tile_len_and_workspace_query():
     assert lib.dsp_chain_path(-1) == prev
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 6) == 48
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 3) == 48   # padded stages
-    assert lib.dsp_chain_tile_len(47996, 71994, 121, 3, 2, 60, 6) == 0    # n_out % 4
+    # n_out % 4 != 0: not k_chain_tile, but the per-phase kernel (chain_pp.h, 6/4's geometry)
+    assert lib.dsp_chain_tile_len(47996, 71994, 121, 3, 2, 60, 6) == 48
+    assert lib.dsp_chain_tile_len(48000, 96000, 81, 2, 1, 40, 6) == 48     # app ratio 2/1
+    assert lib.dsp_chain_tile_len(48000, 24000, 81, 1, 2, 40, 6) == 24     # app ratio 1/2
     assert lib.dsp_chain_tile_len(48000, 52245, 1023, 160, 147, 511, 6) == 32   # generic
     assert lib.dsp_chain_tile_len(48000, 52245, 6401, 160, 147, 3200, 6) == 0   # 41 taps/branch
     assert lib.dsp_chain_tile_len(47999, 52244, 1023, 160, 147, 511, 6) == 0    # n_in % 4
@@ -219,7 +222,8 @@ def _tables_dtype():
                      ("TP", "<f4", (32, 4, 2)), ("geo", "<i4", (6,)), ("cf", "<f8", (6, 4)),
                      ("gain", "<f8"), ("seq", "<f4", (8, 32, 8)), ("adv", "<u4", (8,)),
                      ("classes", "<i4"), ("pad", "<i4"), ("seqs", "<f4", (8, 32, 12)),
-                     ("flush_thr", "<f4"), ("pad3", "<i4", (3,))],
+                     ("flush_thr", "<f4"), ("pad3", "<i4", (3,)), ("tpw", "<f4", (1024,)),
+                     ("pp_td", "<f4"), ("pp_np", "<i4"), ("pp_geo", "<i4"), ("pad4", "<i4")],
                     align=True)
 
 
@@ -318,7 +322,8 @@ def test_chain_tile_tables_host_only():
     X = np.zeros(12)
     for v in y:
         X = A @ X + B * float(v)
-    np.testing.assert_allclose(T @ (G[:48].T @ y), X, rtol=1e-10, atol=1e-12)
+    # (G carries 1 / gain like Q: pass 2 applies the gain at the output)
+    np.testing.assert_allclose(float(tb["gain"]) * (T @ (G[:48].T @ y)), X, rtol=1e-10, atol=1e-12)
     # input-normal pass 1: float32 rows, Q = T^-1 P lower triangular
     Q = tb["Q"]
     Gc = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)   # rows 2j, 2j+1
@@ -366,7 +371,8 @@ def test_chain_tile_tables_host_only():
     X = np.zeros(12)
     for v in y:
         X = A5 @ X + B5 * float(v)
-    np.testing.assert_allclose(tb["T"] @ (tb["G"][:32].T @ y), X, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(float(tb["gain"]) * (tb["T"] @ (tb["G"][:32].T @ y)), X,
+                               rtol=1e-10, atol=1e-12)
     Gc5 = tb["Gc"].astype(np.float64).transpose(0, 2, 1).reshape(64, 12)
     np.testing.assert_allclose(float(tb["gain"]) * (tb["T"] @ (tb["Q"] @ (Gc5[:32].T @ y))), X,
                                rtol=1e-5, atol=1e-6 * np.abs(X).max())

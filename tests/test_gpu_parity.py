@@ -475,12 +475,13 @@ def test_shard_driver_bitwise_invariant(gpu):
 
 
 @pytest.mark.parametrize("n_in,tile", [(48000, True), (4800, True), (96, True), (6144, True),
-                                       (47996, False), (100, False)])
+                                       (47996, True), (100, True), (47999, False)])
 def test_chain_single_pass_matches_two_launch(gpu, n_in, tile):
     """The single-pass chain kernel (csrc/chain_tile.hip) against the
     two-launch chain on the same batch: it is the kernel that ran exactly where
     dsp_chain_tile_len says so (n_out a multiple of 4: one tile, whole tiles,
-    a ragged last tile; otherwise the two-launch chain serves the call), y is
+    a ragged last tile; n_out not a multiple of 4: the per-phase kernel of
+    csrc/chain_pp.h; n_in not a multiple of 4: the two-launch chain), y is
     bitwise the SRC kernel's, z within float64 rounding of the two-launch z
     (other chunking of the same recursion), |X| likewise; rows against the
     reference recipe; the tile hand-off never gave up."""
