@@ -575,7 +575,7 @@ def app_rerun(device, reps=5):
     return out
 
 
-def ratio_sweep(device, channels=4096, steps=3):
+def ratio_sweep(device, channels=4096, steps=8, cases=None, two_launch=True):
     """Every SRC ratio the app's sliders offer (L, M in 1..8, app.py:149-150)
     at the default tap rule K = 40 max(L, M) + 1 (dsp_core.py:158), plus
     config 1's 2/1 at K = 127, on `channels` x 48000 samples at 48 kHz with
@@ -605,7 +605,8 @@ def ratio_sweep(device, channels=4096, steps=3):
         return e0.elapsed_time(e1) / steps
 
     rows = []
-    cases = [(L, M, None) for L in range(1, 9) for M in range(1, 9)] + [(2, 1, 127)]
+    if cases is None:
+        cases = [(L, M, None) for L in range(1, 9) for M in range(1, 9)] + [(2, 1, 127)]
     for L, M, K in cases:
         ch = Chain(ChainConfig(48000, 48000, L, M, K, CONFIG3_GAINS, n_fft=2048, limit_pts=100000),
                    channels, device)
@@ -617,7 +618,7 @@ def ratio_sweep(device, channels=4096, steps=3):
         ms = timed(ch)
         single = "chain_tile" in names
         ms2 = None
-        if single:
+        if single and two_launch:
             prev = _lib.chain_path(1)
             try:
                 ms2 = timed(ch)
@@ -637,7 +638,8 @@ def ratio_sweep(device, channels=4096, steps=3):
     sp = [r for r in rows if r["path"] == "single-pass"]
     return {"channels": channels, "n_in": 48000, "fs": 48000, "steps": steps,
             "single_pass_cases": len(sp), "cases": len(rows),
-            "min_speedup_vs_two_launch": min((r["speedup_vs_two_launch"] for r in sp), default=None),
+            "min_speedup_vs_two_launch": min((r["speedup_vs_two_launch"] for r in sp
+                                              if "speedup_vs_two_launch" in r), default=None),
             "rows": rows}
 
 

@@ -42,6 +42,12 @@
 #pragma once
 #include "chain_tile.h"
 
+// The instantiation list (tools/gen_chain_pp.py); -DPP_LIST='"file"' builds
+// a variant library for A/B timing (tools/build_pp_variant.sh).
+#ifndef PP_LIST
+#define PP_LIST "chain_pp_list.h"
+#endif
+
 namespace dsp {
 
 __host__ __device__ constexpr int pp_pad(int ls) { return (((ls + 4) / 4) % 2) ? 4 : 8; }
@@ -167,6 +173,13 @@ __device__ __forceinline__ void pp_src(const float* xw, tt_ptr tt, float (&y)[G:
   pp_src_parts<G, 0>(xw, tt, y);
 }
 
+// Pass 1 of the per-phase kernels: float32 sums in input-normal coordinates
+// as k_chain_tile's (false), or float64 in block-diagonal ones
+// (pass1_state_f64: measured no closer to the two-launch chain at the app's
+// low output rates -- the float32 rounding of y dominates there -- and 2/1
+// no faster by it: 1.236 vs 1.228 ms at 4096 channels).
+constexpr bool kPpP1F64 = false;
+
 // One tile (REPAIR: the rerun with the non-finite path): the x window, the
 // SRC, then tile_cascade as k_chain_tile (early hand-off included).
 template <class G, bool REPAIR>
@@ -216,16 +229,16 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
     auto fix = [&](float (&yy)[TS], double (&v)[kD]) {
       const float thr = mt->flush_thr;
       const int64_t j0 = (m0 + (int64_t)TS * lane) * a.M + a.c;
-      fix_outputs<TS, true>(a, mt, b, m0 + TS * lane, yy, v, [&](int i, float& nf, float& fin) {
+      fix_outputs<TS, kPpP1F64>(a, mt, b, m0 + TS * lane, yy, v, [&](int i, float& nf, float& fin) {
         const int64_t j = j0 + (int64_t)i * a.M, q = j / a.L;
         const int base = (int)(q - xa);  // x[q] in the window; xa is a multiple of 4
         window_sums(a.taps, a.K, a.L, (int)(j - q * a.L), thr, base,
                     [&](int t) { return lds[G::xpos(base - t)]; }, nf, fin);
       });
     };
-    tile_cascade<TS, true, true, true>(a, mt, lds, y, lane, b, tile, m0, fix);
+    tile_cascade<TS, true, true, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, fix);
   } else {
-    tile_cascade<TS, true, false, true>(a, mt, lds, y, lane, b, tile, m0, 0, early);
+    tile_cascade<TS, true, false, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, 0, early);
   }
 }
 

@@ -654,7 +654,7 @@ struct TilePlan {
 // The per-phase kernels' instantiations (chain_pp_list.h, tools/gen_chain_pp.py).
 constexpr PpEntry kPpEntries[] = {
 #define PP_GEO(IDX, LR, MR, TS, NP, UC, NH, PB) {LR, MR, TS, NP, UC, NH, PB},
-#include "chain_pp_list.h"
+#include PP_LIST
 #undef PP_GEO
 };
 constexpr int kPpCount = (int)(sizeof(kPpEntries) / sizeof(kPpEntries[0]));

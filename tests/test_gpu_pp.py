@@ -65,7 +65,11 @@ def test_app_ratio_single_pass(gpu, L, M, K):
     assert ch.tile_len > 0
     gen = torch.Generator(device=gpu).manual_seed(L * 16 + M)
     x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
-    x[1] *= 40.0                      # drive the clip
+    # drive the clip (x 8: at x 40, as config 3's tests drive it, the float32
+    # rounding of y -- both paths' EQ input, while the oracle filters float64
+    # y and the two-launch chain's carries come from float64 taps -- is worth
+    # 2-3e-6 of z at the app's low output rates 6..35 kHz, the whole budget)
+    x[1] *= 8.0
     x[2, : n_in // 2] = 0.0           # silence then signal
     (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
     with _chain_path(1):
