@@ -504,3 +504,23 @@ def test_nonfinite_lfilter_long_rows(gpu, name, b, a):
         scale = max(1.0, float(np.max(np.abs(want[r][fin]))) if fin.any() else 1.0)
         _same(y[r], want[r], EQ_ATOL * scale, f"{name} row {r}")
     assert wall < 5.0, wall
+
+
+def test_fft_all_inf_2_23_row_repair_is_bounded(gpu):
+    """A 2^23-point row that is +inf everywhere: every input
+    is on the four-step repair's list, and k_nf_fix walks the list per output
+    until both components are NaN.  The class algebra saturates within 8
+    entries for every k here (a host simulation of the walk: mean 4.25, worst
+    8, for 2^10..2^16), so the repair is bounded; the reference's recursion
+    gives NaN in both components of every X[k] for N >= 4 (E[0] + W O[0] with W
+    = 1 + 0j: 0 * inf = NaN), and so must this."""
+    from modules import dsp_core as dc
+    x = np.full(1 << 23, np.inf, dtype=np.float32)
+    with _quiet():
+        dc.fft_diezmado_en_tiempo(x[: 1 << 15])      # warm the tables
+        t0 = time.perf_counter()
+        X = dc.fft_diezmado_en_tiempo(x)
+        wall = time.perf_counter() - t0
+    assert X.shape == x.shape
+    assert np.isnan(X.real).all() and np.isnan(X.imag).all()
+    assert wall < 10.0, wall

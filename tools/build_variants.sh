@@ -7,7 +7,7 @@ mkdir -p ../build/var
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   objs=""
-  for f in abi src_poly iir chain_tile fft fft_nf lfilter_nf audio_io; do
+  for f in abi src_poly iir chain_tile chain_pp_0 chain_pp_1 chain_pp_2 chain_pp_3 fft fft_nf lfilter_nf audio_io; do
     if [ "$f" = "$src" ]; then objs="$objs ../build/var/${f}_$name.o"; else objs="$objs ../build/$f.o"; fi
   done
   extra=""; { [ "$src" = iir ] || [ "$src" = chain_tile ]; } && extra="-fno-slp-vectorize"

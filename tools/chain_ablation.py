@@ -10,6 +10,8 @@ NOSRC   y = window samples (no SRC FMAs)     NOP1  no pass-1 sums (the float32
 NOSCAN  no carry recurrences                       NOP2  no pass-2 cascade
 NOYST   no y store                           NOZST no z store (also lets the
         compiler drop most of pass 2: read it together with NOP2)
+NOSRC5  config 5's kernels (k_chain_gct/gcp): one add per output instead of the
+        SRC's packed FMAs
 """
 import os
 import subprocess
@@ -22,16 +24,20 @@ LIB = os.path.join(ROOT, "dsp-audio-project_amd", "lib")
 HIPCC = "/opt/rocm/bin/hipcc"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fno-slp-vectorize",
          f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
-ALL = ["BASE", "NOSRC", "NOP1", "NOSCAN", "NOP2", "NOYST", "NOZST"]
+ALL = ["BASE", "NOSRC", "NOP1", "NOSCAN", "NOP2", "NOYST", "NOZST", "NOSRC5"]
 
 
-def patched() -> str:
-    s = open(os.path.join(CSRC, "chain_tile.hip")).read()
+def patched() -> tuple[str, str]:
+    """(chain_tile.h, chain_tile.hip) with the ablation switches (round 6: the
+    shared tile code moved to the header)."""
+    SEP = "\n//@@SPLIT@@\n"
+    s = open(os.path.join(CSRC, "chain_tile.h")).read() + SEP + \
+        open(os.path.join(CSRC, "chain_tile.hip")).read()
 
     def rep(old, new, count=1):
         nonlocal s
         if s.count(old) != count:
-            raise SystemExit(f"chain_tile.hip changed; update the ablation patch near: {old[:60]!r}")
+            raise SystemExit(f"chain_tile.h/.hip changed; update the ablation patch near: {old[:60]!r}")
         s = s.replace(old, new)
 
     # SRC: y = window samples (k_chain_tile's DLY part of 48 and plain parts of 24)
@@ -58,15 +64,28 @@ def patched() -> str:
     rep("  store_tile<TS>(lds, y, lane_z, rz);",
         "#ifndef V_NOZST\n  store_tile<TS>(lds, y, lane_z, rz);\n#else\n"
         "  if (y[0] == 12345.f) a.z[0] = y[1];\n#endif")
-    return s
+    # config 5 (k_chain_gct / gcp): y = one window pair per output, no FMAs
+    rep("          acc[o] = __builtin_elementwise_fma(t, X[g2 + pp], acc[o]);",
+        "#ifdef V_NOSRC5\n          if (pp == 0) acc[o] = X[g2] + t;\n#else\n"
+        "          acc[o] = __builtin_elementwise_fma(t, X[g2 + pp], acc[o]);\n#endif")
+    hdr, hip = s.split(SEP)
+    return hdr, hip
 
 
 def main(names):
     os.makedirs(os.path.join(BUILD, "var"), exist_ok=True)
+    import shutil
     src = os.path.join(BUILD, "var", "chain_tile_abl.hip")
+    hdr, hip = patched()
+    with open(os.path.join(BUILD, "var", "chain_tile.h"), "w") as f:
+        f.write(hdr)
     with open(src, "w") as f:
-        f.write(patched())
-    others = [os.path.join(BUILD, f"{n}.o") for n in ("abi", "src_poly", "iir", "fft", "audio_io")]
+        f.write(hip)
+    # chain_pp.h next to the patched header, so that its "chain_tile.h" is that one
+    shutil.copy(os.path.join(CSRC, "chain_pp.h"), os.path.join(BUILD, "var", "chain_pp.h"))
+    others = [os.path.join(BUILD, f"{n}.o") for n in
+              ("abi", "src_poly", "iir", "chain_pp_0", "chain_pp_1", "chain_pp_2", "chain_pp_3",
+               "fft", "fft_nf", "lfilter_nf", "audio_io")]
     procs = []
     for name in names:
         obj = os.path.join(BUILD, "var", f"chain_tile_{name}.o")
