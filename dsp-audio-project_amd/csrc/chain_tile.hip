@@ -767,7 +767,12 @@ bool tile_geometry(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, 
 
 bool tile_geometry_any(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S,
                        TilePlan* tp) {
-  if (S < 0 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
+  // S = 0 (the EQ bypassed, or a clip-only EQ): no single-pass kernel.  z is y
+  // (or its clip) there, and the two-launch chain's copy pass is cheaper than
+  // the kernel's identity cascade; it also keeps the bypass's non-finite
+  // semantics (an inf or NaN stays within the SRC's window; the single-pass
+  // repair would carry it into every later state of the padding stages).
+  if (S < 1 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
   if (L == 1 && M == 1) return false;  // SRC bypass: the caller's cascade path
   if (n_in * 4 + 16 >= ((int64_t)1 << 31) || n_out * 4 + 16 >= ((int64_t)1 << 31)) return false;
   const int TT = (K + L - 1) / L;

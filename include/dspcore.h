@@ -222,6 +222,10 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
  *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
  *       with wave-uniform taps: configs 3 and 4), or
+ *   4..48 (ABI 2.6, the per-phase kernels): every reduced ratio L'/M' with
+ *       L', M' <= 8 at the default tap rule K = 40 max(L, M) + 1, i.e. every
+ *       L, M in 1..8 of the reference app's sliders (and 2/1 at K = 127):
+ *       the sub-chunk length depends on L'/M' (DESIGN.md §3.0.8), or
  *   32: any other L/M with ceil(K/L) <= 8, at most 8 branch classes of the
  *       32-output sub-chunk starts (L / gcd(32 M mod L, L)) and four x windows
  *       that fit 64 KB of LDS with the class tables (config 5's 160/147,

@@ -88,28 +88,32 @@ def test_config1_drop_in_end_to_end(gpu):
 
 
 def test_config1_chain_two_launch_bypass(gpu):
-    """Config 1 through Chain.run: the per-phase single-pass kernel (round 6,
-    csrc/chain_pp.h: 2/1 at K = 127, 64 taps per branch) with the EQ bypassed
-    (S = 0, no clip: z == y bitwise), and the two-launch chain
-    (dsp_chain_path(1)): SRC then the S = 0 cascade launch (the bypass copy)
-    then the spectrum -- y bitwise the single-pass y; against the oracle."""
+    """Config 1 through Chain.run: the EQ is bypassed (S = 0), which takes no
+    single-pass kernel (round 6: the two-launch chain's copy pass is cheaper
+    than an identity cascade and keeps the bypass's local inf / NaN), so SRC
+    then the S = 0 cascade launch (the bypass copy, no clip: z == y bitwise)
+    then the spectrum; with the config-3 gains the same geometry (2/1, K =
+    127: 64 taps per branch) takes the per-phase single-pass kernel (csrc/
+    chain_pp.h), whose y is bitwise the two-launch chain's; against the
+    oracle."""
     from dspcore.chain import Chain, ChainConfig
     from oracle import dsp_ref_cpu as orc
     x, fs = _fastcar_stand_in()
     cfg = ChainConfig(x.size, fs, 2, 1, 127, FLAT, n_fft=1024, limit_pts=100000)
     ch = Chain(cfg, 2, gpu)
-    assert ch.tile_len == 48 and ch.eq.bypass and ch.sos.shape[0] == 0
+    assert ch.tile_len == 0 and ch.eq.bypass and ch.sos.shape[0] == 0
     xs = torch.from_numpy(np.stack([x, -x])).to(gpu)
-    (y1, z1, m1), names1 = _traced(lambda: ch.run(xs))
-    assert names1[:2] == ["chain_tile", "chain_repair"], names1
-    assert torch.equal(y1, z1)
-    with _chain_path(1):
-        (y, z, mag), names = _traced(lambda: ch.run(xs))
+    (y, z, mag), names = _traced(lambda: ch.run(xs))
     # S = 0: one copy pass; no clip, so z may carry infs and the spectrum's
     # non-finite repair follows it (csrc/fft_nf.hip)
     assert names == ["src_poly", "iir_apply", "spectrum", "spectrum_nf"], names
-    assert torch.equal(y, z) and torch.equal(y, y1)
-    assert (m1 - mag).abs().max().item() <= CHAIN_MAG_RTOL * mag.abs().max().item()
+    assert torch.equal(y, z)
+    cfg3 = ChainConfig(x.size, fs, 2, 1, 127, orc.CONFIG3_GAINS, n_fft=1024, limit_pts=100000)
+    ch3 = Chain(cfg3, 2, gpu)
+    assert ch3.tile_len == 48
+    (y3, _, _), names3 = _traced(lambda: ch3.run(xs))
+    assert names3[:2] == ["chain_tile", "chain_repair"], names3
+    assert torch.equal(y3, y)
     ry, rz, _, rm, _ = orc.chain(x, fs, 2, 1, FLAT, 127, 1024, limit_pts=100000)
     y, mag = y.cpu().numpy(), mag.cpu().numpy()
     assert np.max(np.abs(y[0] - ry)) <= SRC_ATOL
