@@ -136,11 +136,6 @@ struct TileTables {
   alignas(16) float tpw[kPpTapFloats];
   float pp_td;
   int32_t pp_np, pp_geo, pad4;
-  // Stage 0 as a float32 TPT state-variable section (round 6 A/B, variant
-  // builds with -DDSP_SVF0=1; chain_tile.hip svf_tables): {A1, A2, A3, m0, m1,
-  // m2} and the DF2 -> SVF state map (row-major 2x2, float64).
-  float svf[8];
-  double svfM[4];
 };
 
 struct TileArgs {
@@ -541,16 +536,6 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
   // states are in those coordinates), and z = fl32(v) * gain32 -- one float32
   // multiply per sample instead of a float64 one (two roundings: <= 1.5 ulp).
   const float g32 = (float)mt->gain;
-#if DSP_SVF0
-  // stage 0 as a float32 TPT state-variable section (Simper/Zavalishin):
-  // v3 = u - s1, (v1, v2) = (A1 s0, s1 + A2 s0) + (A2, A3) v3,
-  // (s0, s1) <- 2 (v1, v2) - (s0, s1), out = m0 u + m1 v1 + m2 v2; its state
-  // from the DF2 one by the host's 2x2 map
-  f32x2 svs = f32x2{(float)fma(mt->svfM[1], s2[0], mt->svfM[0] * s1[0]),
-                    (float)fma(mt->svfM[3], s2[0], mt->svfM[2] * s1[0])};
-  const f32x2 sA12 = f32x2{mt->svf[0], mt->svf[1]}, sA23 = f32x2{mt->svf[1], mt->svf[2]};
-  const float sm0 = mt->svf[3], sm1 = mt->svf[4], sm2 = mt->svf[5];
-#endif
   {
     double pend[kS];  // pend[k]: stage k's output from the previous step
 #pragma unroll
@@ -559,17 +544,6 @@ __device__ __forceinline__ void pass2_cascade(const TileArgs& a, tt_ptr mt, floa
       for (int k = kS - 1; k >= 0; --k) {
         const int t = st - k;
         if (t < 0 || t >= TS) continue;
-#if DSP_SVF0
-        if (k == 0) {
-          const float u0 = y[t];
-          const float v3 = u0 - svs.y;
-          const f32x2 p = __builtin_elementwise_fma(sA12, f32x2{svs.x, svs.x}, f32x2{0.f, svs.y});
-          const f32x2 v = __builtin_elementwise_fma(sA23, f32x2{v3, v3}, p);
-          svs = __builtin_elementwise_fma(f32x2{2.f, 2.f}, v, -svs);
-          pend[0] = (double)fmaf(sm2, v.y, fmaf(sm1, v.x, sm0 * u0));
-          continue;
-        }
-#endif
         const double u = k == 0 ? (double)y[t] : pend[k - 1];
         const double c1 = mt->cf[k][0], c2 = mt->cf[k][1], a1 = mt->cf[k][2], a2 = mt->cf[k][3];
         const double w = fma(-a2, s2[k], fma(-a1, s1[k], u));

@@ -1195,49 +1195,6 @@ bool pp_rows(const float* taps, int K, int L, int M, int64_t c, const PpEntry& e
   return true;
 }
 
-// Stage 0 of the cascade as a TPT state-variable section (the -DDSP_SVF0=1
-// A/B build): coefficients from the DF2 row {1, c1, c2; 1, a1, a2} (the
-// bilinear peaking section: g^2 = (1 + a1 + a2) / (1 - a1 + a2), tools/
-// sim_mixed_precision.py svf_32) and the map M of DF2 states (w1, w2) to SVF
-// states, M = O_s^-1 O_d from the two observability matrices.
-void svf_tables(const double* c, TileTables* tt) {
-  const double c1 = c[1], c2 = c[2], a1 = c[3], a2 = c[4];
-  const double g2 = (1 + a1 + a2) / (1 - a1 + a2);
-  if (!(g2 > 0) || !(1 + a2 != 0)) return;
-  const double g = std::sqrt(g2), D0 = 2 * (1 + g2) / (1 + a2), gk = D0 - 1 - g2, kk = gk / g;
-  const double N[3] = {D0, c1 * D0, c2 * D0};
-  double Mx[3][3] = {{1 + gk + g2, g, g2}, {2 * g2 - 2, 0.0, 2 * g2}, {1 - gk + g2, -g, g2}};
-  // solve Mx m = N (Cramer)
-  auto det3 = [](double m[3][3]) {
-    return m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
-           m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
-           m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
-  };
-  const double d = det3(Mx);
-  double m[3];
-  for (int j = 0; j < 3; ++j) {
-    double t[3][3];
-    for (int r = 0; r < 3; ++r)
-      for (int q = 0; q < 3; ++q) t[r][q] = q == j ? N[r] : Mx[r][q];
-    m[j] = det3(t) / d;
-  }
-  const double A1 = 1 / (1 + g * (g + kk)), A2 = g * A1, A3 = g * A2;
-  // state-space forms: DF2 x = (w1, w2), SVF s = (s0, s1)
-  const double Ad[2][2] = {{-a1, -a2}, {1, 0}}, Cd[2] = {c1 - a1, c2 - a2};
-  const double As[2][2] = {{2 * A1 - 1, -2 * A2}, {2 * A2, 1 - 2 * A3}};
-  const double Cs[2] = {m[1] * A1 + m[2] * A2, -m[1] * A2 + m[2] * (1 - A3)};
-  const double Od[2][2] = {{Cd[0], Cd[1]},
-                           {Cd[0] * Ad[0][0] + Cd[1] * Ad[1][0], Cd[0] * Ad[0][1] + Cd[1] * Ad[1][1]}};
-  const double Os[2][2] = {{Cs[0], Cs[1]},
-                           {Cs[0] * As[0][0] + Cs[1] * As[1][0], Cs[0] * As[0][1] + Cs[1] * As[1][1]}};
-  const double ds = Os[0][0] * Os[1][1] - Os[0][1] * Os[1][0];
-  const double Oi[2][2] = {{Os[1][1] / ds, -Os[0][1] / ds}, {-Os[1][0] / ds, Os[0][0] / ds}};
-  for (int r = 0; r < 2; ++r)
-    for (int q = 0; q < 2; ++q) tt->svfM[2 * r + q] = Oi[r][0] * Od[0][q] + Oi[r][1] * Od[1][q];
-  const double co[6] = {A1, A2, A3, m[0], m[1], m[2]};
-  for (int i = 0; i < 6; ++i) tt->svf[i] = (float)co[i];
-}
-
 // Key of tables whose taps take the DLY kernel (never 0, never the plain key).
 uint64_t dly_key(uint64_t base) {
   const uint64_t k = base ^ 0x9e3779b97f4a7c15ull;
@@ -1316,7 +1273,6 @@ int chain_tile_tables(void* out, size_t out_bytes, int64_t n_in, int64_t n_out, 
     tt->cf[k][3] = p.c[k][4];
   }
   tt->gain = p.G;
-  if (S > 0) svf_tables(p.c[0], tt);
   // pass 2 applies the gain at the output (pass2_cascade): states in 1 / gain
   // (Q for the float32 pass 1, G for the float64 one of the per-phase kernels)
   for (int r = 0; r < kD; ++r)

@@ -223,8 +223,7 @@ def _tables_dtype():
                      ("gain", "<f8"), ("seq", "<f4", (8, 32, 8)), ("adv", "<u4", (8,)),
                      ("classes", "<i4"), ("pad", "<i4"), ("seqs", "<f4", (8, 32, 12)),
                      ("flush_thr", "<f4"), ("pad3", "<i4", (3,)), ("tpw", "<f4", (1024,)),
-                     ("pp_td", "<f4"), ("pp_np", "<i4"), ("pp_geo", "<i4"), ("pad4", "<i4"),
-                     ("svf", "<f4", (8,)), ("svfM", "<f8", (4,))],
+                     ("pp_td", "<f4"), ("pp_np", "<i4"), ("pp_geo", "<i4"), ("pad4", "<i4")],
                     align=True)
 
 
