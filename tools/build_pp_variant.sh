@@ -2,8 +2,8 @@
 # (A/B timing of k_chain_pp geometries with tools/gpu_libs.sh or ratio timing):
 #   bash tools/build_pp_variant.sh NAME LIST_FILE
 set -e
-cd "$(dirname "$0")/../dsp-audio-project_amd/csrc"
 name=$1; list=$(realpath "$2")
+cd "$(dirname "$0")/../dsp-audio-project_amd/csrc"
 mkdir -p ../build/var
 flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -I. -fno-slp-vectorize -DPP_LIST=\"$list\""
 objs=""
