@@ -383,14 +383,20 @@ __device__ __forceinline__ void store_tile(float* lds, const float (&v)[TS], int
       // output float g = 4 (lane + 64 k) sits in row r = g div TS at r RS + g
       // mod TS = g + 4 r (StageBase)
       const int g = 4 * (lane + kWave * k);
-      if (NF4 % kWave && k == NR - 1 && lane + kWave * k >= NF4) continue;
+      // A partial last round (TS not a multiple of 8: the per-phase kernels)
+      // stores from every lane, those past the half's outputs at an offset the
+      // resource drops: no branch, so the y stores a counted hand-off wait
+      // relies on (tile_cascade, vmcnt(TS / 4) <= 2 NR) are issued on every
+      // path (tools/isa_count.py --check-handoff).
+      const bool past = NF4 % kWave && k == NR - 1 && lane + kWave * k >= NF4;
       const float4 f = *reinterpret_cast<const float4*>(lds + sb.at(k));
       u32x4 d;
       d.x = __float_as_uint(f.x);
       d.y = __float_as_uint(f.y);
       d.z = __float_as_uint(f.z);
       d.w = __float_as_uint(f.w);
-      __builtin_amdgcn_raw_buffer_store_b128(d, rs, (h * (kWave / 2) * TS + g) * 4, 0, kStream);
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, past ? 0x7ffffff0 : (h * (kWave / 2) * TS + g) * 4,
+                                             0, kStream);
     }
   }
   fence();

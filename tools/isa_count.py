@@ -7,7 +7,7 @@ maintenance): a quick check of what a source change did to a kernel.
     python tools/isa_count.py --check-handoff file.s
 
 --check-handoff (run by __graft_entry__.build()): the single-pass chain kernels
-(k_chain_tile, k_chain_gct, k_chain_gen; not their rare-path repair kernels,
+(k_chain_tile, k_chain_gct, k_chain_gen, k_chain_pp; not their rare-path repair kernels,
 whose timing does not matter) must issue their SRC and pass-1 work
 before the tile hand-off wait (csrc/chain_tile.hip, tile_cascade): no
 v_pk_fma_f32 (the SRC's and pass 1's packed FMAs) after the poll loop's first
@@ -130,7 +130,7 @@ def check_handoff(path, text=None):
     heads = [(m.start(), m.group(1)) for m in re.finditer(r"^(_Z\w+):", s, re.M)]
     bad, seen, report = [], 0, []
     for i, (pos, name) in enumerate(heads):
-        if not re.search(r"k_chain_(tile|gct|gen)", name) or "_repair" in name:
+        if not re.search(r"k_chain_(tile|gct|gen|pp)", name) or "_repair" in name:
             continue
         seen += 1
         end = heads[i + 1][0] if i + 1 < len(heads) else len(s)
