@@ -12,9 +12,10 @@ state -- wrong z, and no give-up to report it.  So after every replay:
   * spot rows are within the parity tolerances of the oracle
     (reference dsp_core.py:133-254 for y and z, :68-98 for |X|);
   * the workspace's status word and its whole flag array read zero.
-Three geometries: config 3 at full size (k_chain_tile, 4096 channels x 24
-tiles: many dispatch generations), config 5 at full size (the persistent
-k_chain_gcp<160, 147>) and the config-4 kernel at 16384 channels.
+Geometries: config 3 at full size (k_chain_tile, 4096 channels x 24 tiles:
+many dispatch generations), config 5 at full size (the persistent
+k_chain_gcp<160, 147>), the config-4 kernel at 16384 channels, and two of the
+app's ratios on the per-phase kernels (2/1 and 3/4, 4096 channels).
 """
 import numpy as np
 import pytest
@@ -53,6 +54,9 @@ def _workspace_clear(ch):
     ("config3", 4096, 48000, 3, 2, None, (0, 2047, 4095)),
     ("config5", 8192, 44100, 160, 147, 1023, (0, 8191)),
     ("config4-kernel", 16384, 48000, 3, 2, None, (0, 16383)),
+    # the per-phase kernels (csrc/chain_pp.h): an app ratio up and one down
+    ("ratio-2/1", 4096, 48000, 2, 1, None, (0, 4095)),
+    ("ratio-3/4", 4096, 48000, 3, 4, None, (0, 4095)),
 ])
 def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
     from dspcore.chain import Chain, ChainConfig
@@ -65,7 +69,9 @@ def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
     xs = []
     for r in range(3):
         x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
-        x[r] *= 40.0                       # a clipped row, a different one per replay
+        # a clipped row, a different one per replay (x 8 at the app's ratios:
+        # tests/test_gpu_pp.py says why)
+        x[r] *= 8.0 if tag.startswith("ratio") else 40.0
         xs.append(x)
     # eager reference runs (hand-off status checked after each)
     eager = []
