@@ -218,7 +218,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * result is bitwise independent of B.
  *
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
- * S <= 6 with every b0 != 0, n_in a multiple of 4, not the SRC bypass, and
+ * 1 <= S <= 6 with every b0 != 0 (ABI 2.6: S = 0, the EQ bypassed, takes the
+ * two-launch chain's copy pass), n_in a multiple of 4, not the SRC bypass, and
  *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
  *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
  *       with wave-uniform taps: configs 3 and 4), or
