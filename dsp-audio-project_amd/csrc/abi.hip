@@ -82,7 +82,9 @@ int dsp_version(void) {
   // 2.5.0: DSP_MAX_LOG2N_FFT 28 -> 30 (nested four-step, round 5).
   // 2.6.0: dsp_lfilter_nonfinite_f32 scans x for a / a0 = [1, 0, ...];
   // single-pass chain kernels for every app ratio (round 6).
-  return 20600;
+  // 2.7.0: dsp_chain_f32 takes the SRC bypass as the one-tap SRC (L = M = 1,
+  // K = 1) single-pass, and mag == NULL skips the spectrum (round 6).
+  return 20700;
 }
 
 const char* dsp_last_error(void) { return dsp::g_error.c_str(); }
@@ -273,6 +275,7 @@ int dsp_chain_f32(const float* x, float* y, float* z, float* mag, int64_t B, int
                               state_table, scratch_bytes ? scratch : nullptr, scratch_bytes, s);
   }
   if (rc) return rc;
+  if (!mag) return DSP_OK;  // (ABI 2.7) no spectrum asked for
   // after the clip z holds no inf, and NaN alone gives every bin NaN as in the
   // reference: the non-finite repair runs only when the cascade does not clip
   return dsp::launch_spectrum(z, mag, B, ld_y, seg_start, seg_len, log2n, ld_mag, window,

@@ -25,6 +25,12 @@
 // summation order of k_src_reg / k_src_generic (src_poly.hip), so y is
 // bitwise the two-launch chain's.
 //
+// The cascade alone (ratio 1/1 at K = 1, chain_pp_list.h entry 0): the SRC
+// bypass (dsp_core.py:144-145) as the one-tap SRC y = 1.0 x, every output a
+// delay output, the lane windows back to back (LS = TS): x is read once and z
+// written once, y (= x) never stored -- sistema_ecualizador (dsp_core.py:
+// 216-254) in one pass instead of the two-pass cascade's x read twice.
+//
 // Delay branch (upsampling ratios, UC >= 0).  With wc = 1/L (dsp_core.py:155
 // for L >= M) sinc(n / L) vanishes at every n = k L, so the branch of the
 // centre tap -- slots i = 0 mod L' -- holds that tap alone once the library
@@ -74,8 +80,17 @@ struct PpGeo {
   static constexpr int xpos(int g) { return g + PAD * (g / LS); }   // padded LDS float
   static constexpr int XF = xpos(NWIN + 4) + 4;  // (+4: a part's last float4 may reach past W)
   static constexpr int SF = staging_floats(TS);
-  static constexpr int LDSF0 = XF > SF ? XF : SF;
+  // The one-tap SRC bypass (the cascade alone): lane windows back to back,
+  // every window sample an output.  Its single-pass kernel stages the tile's
+  // x through LDS in two halves of 32 lane windows (XH floats), so that its
+  // LDS fits 4 waves per SIMD; the repair kernel keeps the whole window.
+  static constexpr bool IDENT = LR == 1 && MR == 1 && NP == 1 && UC == 0;
+  static_assert(!IDENT || (W == TS && LS == TS), "bypass windows back to back");
+  static constexpr int XH = (kWave / 2) * LSP;
+  static constexpr int LDSF0 = (IDENT ? XH : XF) > SF ? (IDENT ? XH : XF) : SF;
   static constexpr int LDSF = (LDSF0 > kScanFloats ? LDSF0 : kScanFloats) + 3 & ~3;
+  static constexpr int LDSR0 = XF > SF ? XF : SF;  // repair kernel
+  static constexpr int LDSR = (LDSR0 > kScanFloats ? LDSR0 : kScanFloats) + 3 & ~3;
 };
 
 // SRC outputs H0 .. H0+NH-1 of the lane's sub-chunk (the non-delay ones),
@@ -154,10 +169,11 @@ __device__ __forceinline__ void pp_src(const float* xw, tt_ptr tt, float (&y)[G:
     const float td = tq->pp_td;
 #pragma unroll
     for (int i = 0; i < G::TS; i += G::LR) y[i] = td * xw[G::xpos(G::Qc(i) + G::UC)];
-    if constexpr (G::LR == 1) {
+    if constexpr (G::LR == 1 && G::W > G::TS) {
       // every output a delay output (L = M): no FMA meets the rest of the
       // window, so an inf or NaN there would not reach the tile's end state
-      // and the repair kernel.  Flag it (fma(x, 0, acc) is NaN exactly for a
+      // and the repair kernel.  (W == TS: the one-tap SRC bypass, whose
+      // outputs are the whole window, needs no flag.)  Flag it (fma(x, 0, acc) is NaN exactly for a
       // non-finite x): y[0] becomes NaN, the repair reruns the channel and
       // recomputes every output with the reference's semantics.
       f32x2 acc = {0.f, 0.f};
@@ -194,7 +210,44 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
   // its first sample xa = tile * 64 LS + cq is a multiple of 4 (the host's
   // alignment A went into the tap rows)
   const int64_t xa = tile * (int64_t)(kWave * G::LS) + a.cq;
-  {
+  float y[TS];
+  if constexpr (G::IDENT && !REPAIR) {
+    // the cascade alone: all 12 float4 loads of the lane in flight at once
+    // (float4 f = lane + 64 k of the tile's 64 TS samples, coalesced), then
+    // the two halves through LDS, each read back by its 32 lanes as their
+    // y = td x (td = 1.0 for the bypass)
+    static_assert(TS == 48 && G::XH <= G::LDSF, "two halves of 32 x 48 samples");
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
+    constexpr int NF = kWave * TS / 4 / kWave;  // float4s per lane: 12
+    f32x4 v[NF];
+    const int off0 = (int)(xa * 4) + 16 * lane;
+#pragma unroll
+    for (int k = 0; k < NF; ++k)
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(rx, off0 + 1024 * k, 0, kStream);
+    tt_ptr tq = mt;
+    asm volatile("" : "+s"(tq));
+    const float td = tq->pp_td;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int k = 0; k < NF / 2; ++k)
+        *reinterpret_cast<f32x4*>(lds + G::xpos(4 * (lane + kWave * k))) = v[h * (NF / 2) + k];
+      fence();
+      if ((lane >> 5) == h) {
+        const float* xw = lds + G::LSP * (lane & 31);
+#pragma unroll
+        for (int j = 0; j < TS / 4; ++j) {
+          const f32x4 f = *reinterpret_cast<const f32x4*>(xw + 4 * j);
+          y[4 * j] = td * f.x;
+          y[4 * j + 1] = td * f.y;
+          y[4 * j + 2] = td * f.z;
+          y[4 * j + 3] = td * f.w;
+        }
+      }
+      fence();
+    }
+  } else {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.x) + b * a.ld_x, 0, (int)(a.n_in * 4), 0x00020000);
     constexpr int NF = G::NWIN / 4;
@@ -208,8 +261,8 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
         *reinterpret_cast<f32x4*>(lds + G::xpos(4 * f)) = v;
       }
     }
+    fence();  // one wave: its LDS operations execute in order
   }
-  fence();  // one wave: its LDS operations execute in order
   EarlyEntry early{false, reinterpret_cast<const double*>(lds + G::LDSF)};
   if (!REPAIR && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
     early.early = true;
@@ -222,8 +275,7 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
     }
   }
   // ---- 1. SRC
-  float y[TS];
-  pp_src<G>(lds + G::LSP * lane, mt, y);
+  if constexpr (!G::IDENT || REPAIR) pp_src<G>(lds + G::LSP * lane, mt, y);
   pin(y);
   if constexpr (REPAIR) {
     auto fix = [&](float (&yy)[TS], double (&v)[kD]) {
@@ -251,7 +303,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 
 template <class G>
 __global__ __launch_bounds__(kWave) void k_chain_pp_repair(TileArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[G::LDSF + 2 * kD];
+  __shared__ __attribute__((aligned(16))) float lds[G::LDSR + 2 * kD];
   repair_channels(a, 0, 1, [&](int64_t b, int64_t tile) {
     chain_pp_body<G, true>(a, lds, (int)threadIdx.x, b, tile);
   });

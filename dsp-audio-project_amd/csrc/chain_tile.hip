@@ -773,7 +773,10 @@ bool tile_geometry_any(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t
   // semantics (an inf or NaN stays within the SRC's window; the single-pass
   // repair would carry it into every later state of the padding stages).
   if (S < 1 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
-  if (L == 1 && M == 1) return false;  // SRC bypass: the caller's cascade path
+  // SRC bypass (L = M = 1): only as the one-tap SRC (K = 1, c = 0; the
+  // caller passes the tap 1.0), which the per-phase entry of the cascade alone
+  // serves (chain_pp.h); any other L = M = 1 call takes the two-launch chain.
+  if (L == 1 && M == 1 && (K != 1 || c != 0)) return false;
   if (n_in * 4 + 16 >= ((int64_t)1 << 31) || n_out * 4 + 16 >= ((int64_t)1 << 31)) return false;
   const int TT = (K + L - 1) / L;
   // Specialised kernel: lane windows on 16-byte boundaries, i.e. the x offset

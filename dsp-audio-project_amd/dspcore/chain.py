@@ -75,8 +75,13 @@ class Chain:
         self.device = torch.device(device)
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        self.src: SrcPlan = src_plan(cfg.n_in, cfg.fs, cfg.M, cfg.L, cfg.num_taps)
         self.identity_src = cfg.L == 1 and cfg.M == 1
+        # SRC bypass (dsp_core.py:144-145): y is x itself.  To the library it
+        # is the one-tap SRC y = 1.0 x (K = 1), whose single-pass kernel is
+        # the cascade alone: x read once, z written once (include/dspcore.h).
+        self.src: SrcPlan = (SrcPlan(1, 1, 1, np.ones(1), 0, cfg.n_in, cfg.n_in, cfg.fs)
+                             if self.identity_src else
+                             src_plan(cfg.n_in, cfg.fs, cfg.M, cfg.L, cfg.num_taps))
         n_out = cfg.n_in if self.identity_src else self.src.n_out
         self.n_out = n_out
         self.fs_out = cfg.fs if self.identity_src else self.src.fs_out
@@ -85,7 +90,7 @@ class Chain:
         self.spec: SpectrumPlan = spectrum_plan(spec_len, cfg.n_fft)
         S = self.eq.sos.shape[0]
         lib = _lib.load()
-        self.tile_len = 0 if self.identity_src else int(lib.dsp_chain_tile_len(
+        self.tile_len = 0 if (self.identity_src and self.eq.bypass) else int(lib.dsp_chain_tile_len(
             cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S))
         # Two-launch path (other geometries, or dsp_chain_path(1)): x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
@@ -146,8 +151,9 @@ class Chain:
             else:
                 self.tile_len = 0
         # y: the caller's output, or the two-launch chain's intermediate; with
-        # keep_y=False on the single-pass path it is never allocated.
-        if self.keep_y or self.tile_len == 0:
+        # keep_y=False on the single-pass path it is never allocated, and with
+        # the SRC bypass it is x.
+        if not self.identity_src and (self.keep_y or self.tile_len == 0):
             self._ybuf = torch.empty((self.B, self._ld), dtype=torch.float32, device=dev)
             self.y = self._ybuf[:, :n_out]
         else:
@@ -186,8 +192,10 @@ class Chain:
 
     # -- algorithmic traffic ---------------------------------
     def algorithmic_bytes(self) -> int:
-        """4*N_in + 4*N_out (y) + 4*N_out (z) + 4*(N/2+1) per channel."""
-        per = 4 * self.cfg.n_in + 8 * self.n_out + 4 * (self.spec.n_fft // 2 + 1)
+        """4*N_in + 4*N_out (y) + 4*N_out (z) + 4*(N/2+1) per channel (no y
+        with the SRC bypass: y is x)."""
+        per = (4 * self.cfg.n_in + (4 if self.identity_src else 8) * self.n_out
+               + 4 * (self.spec.n_fft // 2 + 1))
         return per * self.B
 
     def _status(self, reset: bool) -> int:
@@ -231,9 +239,15 @@ class Chain:
         callers that replay graphs or pipeline many calls pass False and call
         check() themselves."""
         x = self.check_input(x)
-        if self.identity_src:
-            # SRC bypass (dsp_core.py:144-145): y is x itself.
-            self.run_stages(x)
+        if self.identity_src and (self.tile_len == 0 or ops.ld(x) % 4 or x.data_ptr() % 16
+                                  or _lib.chain_path() == 1):
+            # SRC bypass (dsp_core.py:144-145) without the single-pass kernel
+            # (the EQ bypassed too, dsp_chain_tile_len 0, rows of x not
+            # 16-byte aligned, or dsp_chain_path(1)): y is x itself, the
+            # cascade runs alone.
+            _, z, _ = self.run_stages(x)
+            if z is not self.z:
+                self.z.copy_(z)         # the EQ bypassed too: z is x (run_stages)
             return (x if self.keep_y else None), self.z, self.mag
         lib = _lib.load()
         sos_ptr = _lib.sos_pointer(self.sos)
@@ -252,12 +266,13 @@ class Chain:
                 self.window.data_ptr(), self.tw.data_ptr(), self.workspace.data_ptr(),
                 self.workspace.numel(), stream.cuda_stream)
             _lib.check(rc, "dsp_chain_f32")
-            self._extra_spectra(x, self.y)
+            self._extra_spectra(x, x if self.identity_src else self.y)
             if check is None:
                 check = self.tile_len > 0 and not torch.cuda.is_current_stream_capturing()
             if check:
                 self.check()
-        return (self.y if self.keep_y else None), self.z, self.mag
+        y = x if self.identity_src else self.y
+        return (y if self.keep_y else None), self.z, self.mag
 
     def run_stages(self, x: torch.Tensor, events: list | None = None):
         """Same pass, one entry point per stage; optional (start, end) event pairs

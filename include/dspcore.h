@@ -208,7 +208,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *   y   = SRC(x)                     (dsp_src_polyphase_f32)
  *   z   = clip(cascade(y))           (dsp_biquad_cascade_f32; S == 0 and
  *                                     clip == 0 is the EQ bypass: z := y)
- *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32)
+ *   mag = |FFT(window * z[seg])|     (dsp_spectrum_f32; ABI 2.7: mag == NULL
+ *                                     skips it)
  * y and z must not alias.  workspace_bytes >= dsp_chain_workspace_bytes();
  * the workspace must be zero-filled before its first use, and every call that
  * completes with status 0 (dsp_chain_status) leaves it ready for the next one,
@@ -219,14 +220,17 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
  * 1 <= S <= 6 with every b0 != 0 (ABI 2.6: S = 0, the EQ bypassed, takes the
- * two-launch chain's copy pass), n_in a multiple of 4, not the SRC bypass, and
+ * two-launch chain's copy pass), n_in a multiple of 4, and
  *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
  *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
  *       with wave-uniform taps: configs 3 and 4), or
  *   4..48 (ABI 2.6, the per-phase kernels): every reduced ratio L'/M' with
  *       L', M' <= 8 at the default tap rule K = 40 max(L, M) + 1, i.e. every
  *       L, M in 1..8 of the reference app's sliders (and 2/1 at K = 127):
- *       the sub-chunk length depends on L'/M' (DESIGN.md §3.0.8), or
+ *       the sub-chunk length depends on L'/M' (DESIGN.md §3.0.8), and
+ *       (ABI 2.7) the SRC bypass as the one-tap SRC -- L = M = 1, K = 1,
+ *       c_offset = 0, taps {1.0f}: y = x, so the kernel is the cascade alone,
+ *       x read once and z written once (pass y = NULL: y is x) -- or
  *   32: any other L/M with ceil(K/L) <= 8, at most 8 branch classes of the
  *       32-output sub-chunk starts (L / gcd(32 M mod L, L)) and four x windows
  *       that fit 64 KB of LDS with the class tables (config 5's 160/147,

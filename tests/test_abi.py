@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.dsp_version() == 20600     # 2.6.0: lfilter relabel scan mode, single-pass ratios (2.5.0: FFT to 2^30)
+    assert lib.dsp_version() == 20700     # 2.7.0: the SRC bypass single-pass, mag may be NULL (2.6.0: single-pass ratios)
     assert isinstance(_lib.last_error(), str)
 
 
@@ -173,6 +173,11 @@ def test_chain_path_tile_len_and_workspace_query():
     assert lib.dsp_chain_tile_len(48000, 52245, 6401, 160, 147, 3200, 6) == 0   # 41 taps/branch
     assert lib.dsp_chain_tile_len(47999, 52244, 1023, 160, 147, 511, 6) == 0    # n_in % 4
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 7) == 0    # > 6 stages
+    # the SRC bypass as the one-tap SRC (ABI 2.7): the cascade alone; any
+    # other L = M = 1 call, or no EQ stage, takes the two-launch chain
+    assert lib.dsp_chain_tile_len(48000, 48000, 1, 1, 1, 0, 6) == 48
+    assert lib.dsp_chain_tile_len(48000, 48000, 41, 1, 1, 20, 6) == 0
+    assert lib.dsp_chain_tile_len(48000, 48000, 1, 1, 1, 0, 0) == 0
     B, n_in, n_out = 4096, 48000, 72000
     tiles = -(-n_out // 3072)
     ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)

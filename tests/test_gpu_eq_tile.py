@@ -1,0 +1,167 @@
+"""The cascade alone through the single-pass kernels (ABI 2.7): the SRC bypass
+L = M = 1 (/root/reference/modules/dsp_core.py:144-145, the app's default
+ratio, app.py:149-150) followed by sistema_ecualizador (:216-254) runs as the
+one-tap SRC y = 1.0 x on the per-phase kernel k_chain_pp<PpGeo<1, 1, 48, 1, 0,
+...>> (csrc/chain_pp.h): x read once, z written once, y never stored (it is x).
+
+Against the two-launch path (Chain.run_stages: the two-pass cascade k_iir_wave
+over y = x) on the same batch: z within 2e-6, |X| within 1e-5 of the largest,
+the same inf / NaN masks; rows against the oracle (dsp_core.py:216-254 and
+:68-98 restated in oracle/dsp_ref_cpu.py) within the parity tolerances; one
+tile, ragged last tiles, a row driven into the clip, a row silent for its
+first half, +-15 dB gain sets (tests/golden/eq.npz), rows of x that are not
+16-byte aligned (the two-pass cascade serves them).
+"""
+import contextlib
+import os
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+EQ_ATOL = 1e-5
+MAG_RTOL = 1e-5
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _traced(fn):
+    from dspcore import _lib
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    try:
+        out = tuple(t.clone() if t is not None else None for t in fn())
+        names = [n for n, _ in _lib.trace_read()]
+    finally:
+        _lib.trace_enable(False)
+    return out, names
+
+
+@contextlib.contextmanager
+def _chain_path(path):
+    from dspcore import _lib
+    prev = _lib.chain_path(path)
+    try:
+        yield
+    finally:
+        _lib.chain_path(prev)
+
+
+@pytest.mark.parametrize("n_in,B", [(48000, 6), (3072, 3), (96, 4), (100, 5), (47996, 4),
+                                    (441000, 3)])
+def test_cascade_alone_single_pass(gpu, n_in, B):
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    fs = 48000
+    n_fft = 4096 if n_in >= 3000 else 128   # (the reference's segment rule: 2^k points)
+    cfg = ChainConfig(n_in, fs, 1, 1, None, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 48 and ch.identity_src
+    gen = torch.Generator(device=gpu).manual_seed(n_in % 1000 + B)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[1] *= 40.0                      # drive the clip
+    x[2, : n_in // 2] = 0.0           # silence then signal
+    (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
+    (y0, z0, m0), names0 = _traced(lambda: ch.run_stages(x))
+    assert "chain_tile" in names1 and not any(n.startswith("iir") for n in names1), names1
+    assert "chain_tile" not in names0, names0
+    assert ch.handoff_ok()
+    assert torch.equal(y1, x) and torch.equal(y0, x)     # y is x (the bypass)
+    assert (z1 - z0).abs().max().item() <= 2e-6
+    assert (m1 - m0).abs().max().item() <= MAG_RTOL * m0.abs().max().item()
+    z, mag = z1.cpu().numpy(), m1.cpu().numpy()
+    assert np.abs(z[1]).max() == 1.0
+    for b in (0, 1, 2, B - 1):
+        xb = x[b].cpu().numpy()
+        ry, rz, _, rmag, _ = orc.chain(xb, fs, 1, 1, orc.CONFIG3_GAINS, None, n_fft)
+        np.testing.assert_array_equal(ry, xb)
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(mag[b] - rmag)) <= MAG_RTOL * np.max(rmag)
+    # without y: the same z, and run() hands back None for y
+    ch2 = Chain(cfg, B, gpu, keep_y=False)
+    y2, z2, m2 = ch2.run(x)
+    assert y2 is None and torch.equal(z2, z1) and torch.equal(m2, m1)
+    # the forced two-launch path is the staged one
+    with _chain_path(1):
+        (y3, z3, m3), _ = _traced(lambda: ch.run(x))
+    assert torch.equal(z3, z0) and torch.equal(m3, m0)
+
+
+def test_cascade_alone_golden_eq_cases(gpu):
+    """Every gain set of tests/golden/eq.npz (the reference's own
+    sistema_ecualizador outputs: config 3's gains, +-15 dB on every band,
+    single bands, the unknown band, g = 0.1 edges, the Nyquist clamp) on its
+    7200-sample x32 through the single-pass cascade where it takes it: within
+    1e-5 of the reference's z32, within 2e-6 of the two-pass cascade, the
+    bypass sets returning x itself."""
+    from conftest import golden, golden_gains
+    from dspcore.chain import Chain, ChainConfig
+    g = golden("eq")
+    x32 = g["x32"]
+    n = x32.size - x32.size % 4
+    x = torch.from_numpy(np.ascontiguousarray(x32[:n])[None, :]).to(gpu)
+    cases = sorted(int(k[6:]) for k in g.keys() if k.startswith("gains_"))
+    served = 0
+    for k in cases:
+        gains, fs = golden_gains(g[f"gains_{k}"]), int(g[f"fs_{k}"])
+        cfg = ChainConfig(n, fs, 1, 1, None, gains, n_fft=8192)
+        ch = Chain(cfg, 1, gpu)
+        (y1, z1, _), names = _traced(lambda: ch.run(x))
+        assert torch.equal(y1, x)
+        ref = g[f"z32_{k}"][:n]
+        if ch.tile_len:
+            served += 1
+            assert "chain_tile" in names, (k, names)
+            _, z0, _ = ch.run_stages(x)
+            assert (z1 - z0).abs().max().item() <= 2e-6, k
+        err = float(np.max(np.abs(z1[0].cpu().numpy() - ref)))
+        assert err <= EQ_ATOL, (k, gains, err)
+    assert served >= 5, served
+
+
+def test_cascade_alone_nonfinite_matches_two_pass(gpu):
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 4, 12000
+    cfg = ChainConfig(n_in, 48000, 1, 1, None, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, B, gpu)
+    gen = torch.Generator(device=gpu).manual_seed(11)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0, 3072] = float("nan")         # a tile's first sample
+    x[1, n_in // 2] = float("inf")
+    x[1, n_in // 2 + 3] = float("-inf")
+    x[2, n_in - 1] = float("-inf")    # the last sample
+    x[3, 0] = float("inf")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        (_, z1, m1), names1 = _traced(lambda: ch.run(x))
+        (_, z0, m0), _ = _traced(lambda: ch.run_stages(x))
+    assert "chain_tile" in names1 and "chain_repair" in names1, names1
+    a, b = z1.cpu().numpy(), z0.cpu().numpy()
+    for f in (np.isnan, np.isposinf, np.isneginf):
+        np.testing.assert_array_equal(f(a), f(b))
+    fin = np.isfinite(b)
+    assert np.max(np.abs(a[fin] - b[fin])) <= 2e-6
+    np.testing.assert_array_equal(np.isnan(m1.cpu().numpy()), np.isnan(m0.cpu().numpy()))
+    # and the oracle's masks (lfilter + np.clip on the row)
+    for r in range(B):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            _, rz, _, _, _ = orc.chain(x[r].cpu().numpy(), 48000, 1, 1, orc.CONFIG3_GAINS, None, 2048)
+        np.testing.assert_array_equal(np.isnan(a[r]), np.isnan(rz))
+
+
+def test_cascade_alone_unaligned_rows_take_two_pass(gpu):
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 3, 9600
+    cfg = ChainConfig(n_in, 48000, 1, 1, None, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, B, gpu)
+    buf = torch.rand((B, n_in + 1), device=gpu) * 2 - 1
+    x = buf[:, 1:]                    # rows 4 bytes past a 16-byte boundary
+    (_, z1, _), names = _traced(lambda: ch.run(x))
+    assert "chain_tile" not in names, names
+    (_, z0, _), _ = _traced(lambda: ch.run(x.contiguous()))
+    assert (z1 - z0).abs().max().item() <= 2e-6

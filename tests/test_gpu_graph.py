@@ -14,8 +14,9 @@ state -- wrong z, and no give-up to report it.  So after every replay:
   * the workspace's status word and its whole flag array read zero.
 Geometries: config 3 at full size (k_chain_tile, 4096 channels x 24 tiles:
 many dispatch generations), config 5 at full size (the persistent
-k_chain_gcp<160, 147>), the config-4 kernel at 16384 channels, and two of the
-app's ratios on the per-phase kernels (2/1 and 3/4, 4096 channels).
+k_chain_gcp<160, 147>), the config-4 kernel at 16384 channels, two of the
+app's ratios on the per-phase kernels (2/1 and 3/4, 4096 channels) and the
+app's default 1/1 (the cascade alone, 4096 channels).
 """
 import numpy as np
 import pytest
@@ -57,6 +58,8 @@ def _workspace_clear(ch):
     # the per-phase kernels (csrc/chain_pp.h): an app ratio up and one down
     ("ratio-2/1", 4096, 48000, 2, 1, None, (0, 4095)),
     ("ratio-3/4", 4096, 48000, 3, 4, None, (0, 4095)),
+    # the SRC bypass: the cascade alone (one-tap SRC, y is x)
+    ("eq-only", 4096, 48000, 1, 1, None, (0, 4095)),
 ])
 def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
     from dspcore.chain import Chain, ChainConfig
@@ -99,7 +102,8 @@ def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
         graph.replay()
         torch.cuda.synchronize(gpu)
         ye, ze, me = eager[i]
-        assert torch.equal(ch.y, ye), (tag, rep, "y")
+        y_now = x_static if ch.identity_src else ch.y   # the bypass: y is x
+        assert torch.equal(y_now, ye), (tag, rep, "y")
         assert torch.equal(ch.z, ze), (tag, rep, "z")
         assert torch.equal(ch.mag, me), (tag, rep, "mag")
         assert _workspace_clear(ch) == (0, 0), (tag, rep)
@@ -109,7 +113,7 @@ def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
             for b in rows:
                 ry, rz, _, rmag, _ = orc.chain(xs[i][b].cpu().numpy(), fs, L, M, orc.CONFIG3_GAINS,
                                                K, n_fft)
-                y = ch.y[b].cpu().numpy()
+                y = y_now[b].cpu().numpy()
                 z = ch.z[b].cpu().numpy()
                 mag = ch.mag[b].cpu().numpy()
                 assert np.max(np.abs(y - ry)) <= SRC_ATOL * max(1.0, np.abs(ry).max())

@@ -7,7 +7,8 @@ sample xa = 64 LS t + xa0, the delay branch's outputs one tap times the
 sample at Qc(i) + UC -- must reproduce the reference's SRC
 (/root/reference/modules/dsp_core.py:133-173; oracle.dsp_ref_cpu.resample)
 for every L, M in 1..8 of the app's sliders (app.py:149-150) at the default
-tap rule and for config 1's 2/1 at K = 127.  This pins the host's slot /
+tap rule, for config 1's 2/1 at K = 127 and for the SRC bypass as the one-tap
+SRC (L = M = 1, K = 1: y = x, dsp_core.py:144-145).  This pins the host's slot /
 shift / alignment algebra independently of the GPU."""
 import math
 import os
@@ -77,7 +78,7 @@ def _model_y(x, plan, tb, entry):
 
 
 CASES = [(L, M, None) for L in range(1, 9) for M in range(1, 9) if (L, M) not in ((1, 1), (3, 2))]
-CASES += [(2, 1, 127)]
+CASES += [(2, 1, 127), (1, 1, 1)]   # (1, 1, 1): the SRC bypass as one tap, the cascade alone
 
 
 @pytest.mark.parametrize("L,M,K", CASES, ids=[f"{L}/{M}" + (f"K{K}" if K else "") for L, M, K in CASES])

@@ -1,0 +1,62 @@
+"""The cascade alone (L = M = 1, config-3 gains): the single-pass one-tap
+kernel (Chain.run) against the two-pass cascade (Chain.run_stages) on the same
+box, HIP-graph replay like bench.py, for the batch shapes given as BxN
+(default 4096x48000 32768x48000 1x441000 1x48000 16x441000).  Prints ms per
+call of each path, the single-pass kernel's algorithmic GB/s (x read + z
+written) and the speedup."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dsp-audio-project_amd"))
+
+from dspcore.chain import Chain, ChainConfig  # noqa: E402
+
+GAINS = {"Sub-Bass": 6, "Bass": -4, "Low Mids": 3, "High Mids": -3, "Presence": 5,
+         "Brilliance": -6}
+
+
+def graph_ms(fn, reps):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]] or \
+        [(4096, 48000), (32768, 48000), (1, 441000), (1, 48000), (16, 441000)]
+    dev = torch.device("cuda", 0)
+    for B, n in shapes:
+        cfg = ChainConfig(n, 48000, 1, 1, None, GAINS, n_fft=4096)
+        ch = Chain(cfg, B, dev, keep_y=False)
+        x = torch.rand((B, n), device=dev) * 2 - 1
+        reps = max(5, min(200, int(2e9 // (B * n * 8))))
+        t1 = graph_ms(lambda: ch.run(x, check=False), reps)
+        t0 = graph_ms(lambda: ch.run_stages(x), reps)
+        ch.check()
+        gbs = B * n * 8 / (t1 * 1e-3) / 1e9
+        print(f"B={B} n={n}: single-pass {t1:.4f} ms ({gbs:.0f} GB/s x+z, "
+              f"{B * n / t1 / 1e6:.1f} G samples/s), two-pass {t0:.4f} ms, x{t0 / t1:.2f} "
+              f"(tile_len {ch.tile_len})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
