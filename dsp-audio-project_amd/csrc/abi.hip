@@ -24,7 +24,8 @@ struct TraceState {
 thread_local TraceState g_trace;
 // dsp_chain_path: 0 single-pass kernel where instantiated (default), 1 always
 // the two-launch chain, 2 / 3 the single-pass path with its chained-tile /
-// persistent kernel (where one is built for the geometry).
+// persistent kernel (where one is built for the geometry), 4 the three-launch
+// mode of the cascade alone (ABI 2.7).
 thread_local int g_chain_path = 0;
 // dsp_chain_spin_limit: polls before a single-pass hand-off wait gives up
 // (2^23 polls with s_sleep 2 between them: ~0.4 s).
@@ -83,7 +84,8 @@ int dsp_version(void) {
   // 2.6.0: dsp_lfilter_nonfinite_f32 scans x for a / a0 = [1, 0, ...];
   // single-pass chain kernels for every app ratio (round 6).
   // 2.7.0: dsp_chain_f32 takes the SRC bypass as the one-tap SRC (L = M = 1,
-  // K = 1) single-pass, and mag == NULL skips the spectrum (round 6).
+  // K = 1) single-pass, and mag == NULL skips the spectrum; dsp_chain_path 4;
+  // dsp_chain_mode (round 6).
   return 20700;
 }
 
@@ -173,7 +175,7 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x, int64_
 
 int dsp_chain_path(int32_t path) {
   dsp::clear_error();
-  if (path < -1 || path > 3) return dsp::set_error(DSP_EINVAL, "chain path %d not in [-1, 3]", path);
+  if (path < -1 || path > 4) return dsp::set_error(DSP_EINVAL, "chain path %d not in [-1, 4]", path);
   const int prev = dsp::g_chain_path;
   if (path >= 0) dsp::g_chain_path = path;
   return prev;
@@ -182,6 +184,11 @@ int dsp_chain_path(int32_t path) {
 int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,
                            int64_t c_offset, int32_t S) {
   return dsp::chain_tile_sub(n_in, n_out, K, L, M, c_offset, S);
+}
+
+int32_t dsp_chain_mode(int64_t B, int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,
+                       int64_t c_offset, int32_t S) {
+  return dsp::chain_mode(B, n_in, n_out, K, L, M, c_offset, S);
 }
 
 size_t dsp_chain_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int32_t K, int32_t L,

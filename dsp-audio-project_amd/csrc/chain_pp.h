@@ -198,14 +198,17 @@ constexpr bool kPpP1F64 = false;
 
 // One tile (REPAIR: the rerun with the non-finite path): the x window, the
 // SRC, then tile_cascade as k_chain_tile (early hand-off included).
-template <class G, bool REPAIR>
+// MODE: 0 the chained hand-off, 1 / 2 launch 1 / 3 of the three-launch mode
+// (chain_tile.h, AggEntry / GivenEntry).
+template <class G, bool REPAIR, int MODE = 0>
 __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int lane, int64_t b,
                                               int64_t tile) {
   constexpr int TS = G::TS;
   const int64_t m0 = tile * G::TILE;
   const tt_ptr mt = (tt_ptr)a.tt;
   uint32_t fl = 0;
-  if (!REPAIR && tile > 0 && lane == 0) fl = load_flag(a.flags + b * a.ntiles + tile - 1);
+  if (!REPAIR && MODE == 0 && tile > 0 && lane == 0)
+    fl = load_flag(a.flags + b * a.ntiles + tile - 1);
   // ---- x window of the tile -> padded LDS image (zeros outside [0, n_in));
   // its first sample xa = tile * 64 LS + cq is a multiple of 4 (the host's
   // alignment A went into the tap rows)
@@ -264,7 +267,7 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
     fence();  // one wave: its LDS operations execute in order
   }
   EarlyEntry early{false, reinterpret_cast<const double*>(lds + G::LDSF)};
-  if (!REPAIR && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
+  if (!REPAIR && MODE == 0 && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
     early.early = true;
     if (lane < 2 * kD) {
       const int64_t prev = b * a.ntiles + tile - 1;
@@ -290,7 +293,12 @@ __device__ __forceinline__ void chain_pp_body(const TileArgs& a, float* lds, int
     };
     tile_cascade<TS, true, true, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, fix);
   } else {
-    tile_cascade<TS, true, false, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, 0, early);
+    if constexpr (MODE == 1)
+      tile_cascade<TS, true, false, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, 0, AggEntry{});
+    else if constexpr (MODE == 2)
+      tile_cascade<TS, true, false, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, 0, GivenEntry{});
+    else
+      tile_cascade<TS, true, false, kPpP1F64>(a, mt, lds, y, lane, b, tile, m0, 0, early);
   }
 }
 
@@ -299,6 +307,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     TileArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[G::LDSF + 2 * kD];  // + the early slot
   chain_pp_body<G, false>(a, lds, threadIdx.x, blockIdx.x, blockIdx.y);
+}
+
+// Launches 1 and 3 of the three-launch mode (the cascade alone).
+template <class G, int MODE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_pp3(
+    TileArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[G::LDSF];
+  chain_pp_body<G, false, MODE>(a, lds, threadIdx.x, blockIdx.x, blockIdx.y);
 }
 
 template <class G>
@@ -314,13 +330,30 @@ struct PpEntry {
   int LR, MR, TS, NP, UC, NH, PB;
 };
 
-// Launches k_chain_pp<G> and its repair kernel on s (the caller checked the
-// geometry, tables and workspace: chain_tile.hip launch_chain_tile).
+// Launch 2 of the three-launch mode (chain_tile.hip): the aggregates in
+// states[] scanned into the tiles' entry states, per channel.
+void launch_tile_carry(const TileArgs& a, int tile_len, hipStream_t s);
+
+// Launches k_chain_pp<G> (three: the three-launch mode, built for the cascade
+// alone) and its repair kernel on s (the caller checked the geometry, tables
+// and workspace: chain_tile.hip launch_chain_tile).
 template <class G>
-int pp_launch(const TileArgs& a, unsigned rgrid, hipStream_t s) {
-  {
+int pp_launch(const TileArgs& a, unsigned rgrid, bool three, hipStream_t s) {
+  const dim3 grid((unsigned)a.B, (unsigned)a.ntiles);
+  if constexpr (G::IDENT) {
+    if (three) {
+      {
+        TraceScope trace("chain_tile_agg", s);
+        hipLaunchKernelGGL((k_chain_pp3<G, 1>), grid, dim3(kWave), 0, s, a);
+      }
+      launch_tile_carry(a, G::TS, s);
+      TraceScope trace("chain_tile", s);
+      hipLaunchKernelGGL((k_chain_pp3<G, 2>), grid, dim3(kWave), 0, s, a);
+    }
+  }
+  if (!G::IDENT || !three) {
     TraceScope trace("chain_tile", s);
-    hipLaunchKernelGGL(k_chain_pp<G>, dim3((unsigned)a.B, (unsigned)a.ntiles), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(k_chain_pp<G>, grid, dim3(kWave), 0, s, a);
   }
   TraceScope trace("chain_repair", s);
   hipLaunchKernelGGL(k_chain_pp_repair<G>, dim3(rgrid), dim3(kWave), 0, s, a);
@@ -331,9 +364,13 @@ int pp_launch(const TileArgs& a, unsigned rgrid, hipStream_t s) {
 // One of the translation units chain_pp_<n>.hip: launches the entry `e`
 // if that unit instantiates it, else kNotFused.
 constexpr int kPpUnits = 4;
-int launch_chain_pp_0(const PpEntry& e, const TileArgs& a, unsigned rgrid, hipStream_t s);
-int launch_chain_pp_1(const PpEntry& e, const TileArgs& a, unsigned rgrid, hipStream_t s);
-int launch_chain_pp_2(const PpEntry& e, const TileArgs& a, unsigned rgrid, hipStream_t s);
-int launch_chain_pp_3(const PpEntry& e, const TileArgs& a, unsigned rgrid, hipStream_t s);
+int launch_chain_pp_0(const PpEntry& e, const TileArgs& a, unsigned rgrid, bool three,
+                       hipStream_t s);
+int launch_chain_pp_1(const PpEntry& e, const TileArgs& a, unsigned rgrid, bool three,
+                       hipStream_t s);
+int launch_chain_pp_2(const PpEntry& e, const TileArgs& a, unsigned rgrid, bool three,
+                       hipStream_t s);
+int launch_chain_pp_3(const PpEntry& e, const TileArgs& a, unsigned rgrid, bool three,
+                       hipStream_t s);
 
 }  // namespace dsp

@@ -667,6 +667,16 @@ struct EarlyEntry {
   bool early;
   const double* slot;
 };
+// The three-launch mode of small batches (round 6; chain_pp.h, the cascade
+// alone): a chained hand-off costs ~2 us per tile, so a channel of many tiles
+// waits ntiles x 2 us however few channels there are.  Instead, launch 1
+// (AggEntry) runs every tile from a zero entry state and publishes only that
+// end state -- the tile's aggregate -- in states[tile]; launch 2
+// (k_tile_carry) scans the aggregates of each channel into the tiles' entry
+// states, in place; launch 3 (GivenEntry) reruns every tile from its entry
+// state and publishes its end state over it (for the repair kernel), no flag.
+struct AggEntry {};
+struct GivenEntry {};
 
 template <int TS, bool YST = true, bool REPAIR = false, bool P1F64 = false, class ONNF,
           class ENTRY = ChainedEntry>
@@ -675,6 +685,8 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
                                              int64_t m0, ONNF&& on_nf, ENTRY&& entry = ENTRY{}) {
   constexpr bool kRegCarry = std::is_same_v<std::decay_t<ENTRY>, RegCarry>;
   constexpr bool kEarly = std::is_same_v<std::decay_t<ENTRY>, EarlyEntry>;
+  constexpr bool kAgg = std::is_same_v<std::decay_t<ENTRY>, AggEntry>;
+  constexpr bool kGiven = std::is_same_v<std::decay_t<ENTRY>, GivenEntry>;
   // ---- 2. pass 1: zero-state end state of the sub-chunk
   double v[kD];
   if constexpr (P1F64) pass1_state_f64<TS>(mt, y, v);
@@ -708,7 +720,16 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
     *reinterpret_cast<f64x2*>(rows + lane * kScanRow + 2 * k) = f64x2{v[2 * k], v[2 * k + 1]};
   // The tile's entry state (hand-off wait; lane 0) goes to the park row
   // (tile 0: zeros, one zero register pair for all six stores).
-  if (tile == 0) {
+  if constexpr (kGiven) {
+    // (launch 2 wrote the entry state over the aggregate)
+    if (lane == 0) {
+      const int64_t me = b * a.ntiles + tile;
+#pragma unroll
+      for (int k = 0; k < kS; ++k)
+        *reinterpret_cast<f64x2*>(park + 2 * k) =
+            *reinterpret_cast<const f64x2*>(a.states + me * kD + 2 * k);
+    }
+  } else if (kAgg || tile == 0) {
     if (lane == 0) {
 #pragma unroll
       for (int k = 0; k < kS; ++k) *reinterpret_cast<f64x2*>(park + 2 * k) = f64x2{0.0, 0.0};
@@ -837,7 +858,8 @@ __device__ __forceinline__ void tile_cascade(const TileArgs& a, tt_ptr mt, float
   // The flag follows once these state stores are acknowledged; the y stores
   // below go out first, so that the wave does not sit in vmcnt(0) on the
   // stores' round trip (round 4): the wait counts the y stores as younger.
-  const bool raise = !kRegCarry && tile + 1 < a.ntiles;
+  if constexpr (kAgg) return;  // launch 1: the aggregate is all it computes
+  const bool raise = !kRegCarry && !kGiven && tile + 1 < a.ntiles;
   auto raise_flag = [&] {
     if (lane == 8 * 7) store_flag(a.flags + b * a.ntiles + tile, 1u);
   };

@@ -1219,11 +1219,99 @@ TileWs tile_ws(int64_t B, int64_t ntiles) {
   return w;
 }
 
+// Launch 2 of the three-launch mode (chain_tile.h, AggEntry): wave k of the
+// channel's workgroup owns state block k; lane l of round r holds tile
+// t = 64 r + l.  With P = D_k^(64 TS) (a tile) and e_t the aggregates, the
+// entry states S_t = sum_(s<t) P^(t-1-s) e_s come from an inclusive
+// Kogge-Stone over the lanes, I_l = sum_(s<=l) P^(l-s) e_(64r+s), and the
+// carry C of the rounds before: S_(64r+l) = P^l C + I_(l-1), C' = P^64 C +
+// I_63.  They replace the aggregates in states[] (launch 3 reads them).
+__global__ __launch_bounds__(kWave * kS) void k_tile_carry(TileArgs a) {
+  typedef double m2[4];  // row-major 2x2
+  auto mul = [](const m2& x, const m2& y, m2& r) {
+    const double r0 = fma(x[0], y[0], x[1] * y[2]), r1 = fma(x[0], y[1], x[1] * y[3]);
+    const double r2 = fma(x[2], y[0], x[3] * y[2]), r3 = fma(x[2], y[1], x[3] * y[3]);
+    r[0] = r0;
+    r[1] = r1;
+    r[2] = r2;
+    r[3] = r3;
+  };
+  const int k = (int)threadIdx.x / kWave;
+  const int lane = (int)threadIdx.x % kWave;
+  const int64_t b = blockIdx.x;
+  const TileTables* mt = a.tt;
+  m2 pw[7];  // P^(2^j)
+  {
+    const m2 d5 = {mt->Dp[5][k][0], mt->Dp[5][k][1], mt->Dp[5][k][2], mt->Dp[5][k][3]};
+    mul(d5, d5, pw[0]);
+  }
+#pragma unroll
+  for (int j = 1; j < 7; ++j) mul(pw[j - 1], pw[j - 1], pw[j]);
+  m2 pl = {1.0, 0.0, 0.0, 1.0};  // P^lane
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    if ((lane >> j) & 1) mul(pl, pw[j], pl);
+  double c0 = 0.0, c1 = 0.0;
+  double* st = a.states + b * a.ntiles * kD + 2 * k;
+  for (int64_t t0 = 0; t0 < a.ntiles; t0 += kWave) {
+    const int64_t t = t0 + lane;
+    const bool in = t < a.ntiles;
+    double i0 = in ? st[t * kD] : 0.0, i1 = in ? st[t * kD + 1] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int d = 1 << j;
+      const int src = lane >= d ? lane - d : lane;
+      const double x0 = shfl_f64(i0, src), x1 = shfl_f64(i1, src);
+      if (lane >= d) {
+        i0 = fma(pw[j][0], x0, fma(pw[j][1], x1, i0));
+        i1 = fma(pw[j][2], x0, fma(pw[j][3], x1, i1));
+      }
+    }
+    double x0 = shfl_f64(i0, lane > 0 ? lane - 1 : 0), x1 = shfl_f64(i1, lane > 0 ? lane - 1 : 0);
+    if (lane == 0) x0 = x1 = 0.0;
+    if (in) {
+      st[t * kD] = fma(pl[0], c0, fma(pl[1], c1, x0));
+      st[t * kD + 1] = fma(pl[2], c0, fma(pl[3], c1, x1));
+    }
+    const double j0 = shfl_f64(i0, kWave - 1), j1 = shfl_f64(i1, kWave - 1);
+    const double n0 = fma(pw[6][0], c0, fma(pw[6][1], c1, j0));
+    const double n1 = fma(pw[6][2], c0, fma(pw[6][3], c1, j1));
+    c0 = n0;
+    c1 = n1;
+  }
+}
+
+// Whether the cascade alone takes the three-launch mode: when the chained
+// hand-off (~2.2 us a tile: one 441000-sample channel, 144 tiles, 0.31 ms)
+// would bound the launch.  Fitted to both modes forced on one box at 1..4096
+// channels of 48000 and 441000 samples (profiles/r06_eq_alone_modes.txt):
+// chained ~ 2.2 us ntiles + 5 ns B ntiles, three launches ~ 15 us + 8.4 ns
+// B ntiles (each tile's x, pass 1 and scan twice; two more launches).
+bool three_launch(int64_t B, int64_t ntiles) {
+  const double tiles = (double)B * (double)ntiles;
+  return 15e-6 + 8.4e-9 * tiles < 2.2e-6 * (double)ntiles + 5e-9 * tiles;
+}
+
 }  // namespace
+
+void launch_tile_carry(const TileArgs& a, int, hipStream_t s) {
+  TraceScope trace("chain_tile_carry", s);
+  hipLaunchKernelGGL(k_tile_carry, dim3((unsigned)a.B), dim3(kWave * kS), 0, s, a);
+}
 
 int64_t chain_tile_sub(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S) {
   TilePlan tp;
   return tile_geometry(n_in, n_out, K, L, M, c, S, &tp) ? tp.tsub : 0;
+}
+
+int chain_mode(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S) {
+  TilePlan tp;
+  if (B < 1 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 0;
+  if (tp.kind == 4) {
+    const PpEntry& e = kPpEntries[tp.pp];
+    if (e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0 && three_launch(B, tp.ntiles)) return 3;
+  }
+  return 1;
 }
 
 size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M,
@@ -1358,10 +1446,14 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const PpNeed n = pp_need(K, L, M, c);
     a.cq = n.xa0;
     const PpEntry& e = kPpEntries[tp.pp];
-    int rc = launch_chain_pp_0(e, a, rgrid, s);
-    if (rc == kNotFused) rc = launch_chain_pp_1(e, a, rgrid, s);
-    if (rc == kNotFused) rc = launch_chain_pp_2(e, a, rgrid, s);
-    if (rc == kNotFused) rc = launch_chain_pp_3(e, a, rgrid, s);
+    // the cascade alone (the one-tap SRC bypass): the three-launch mode for
+    // small batches of long rows (variant 4 forces it, 2 the chained tiles)
+    const bool ident = e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0;
+    const bool three = ident && variant != 2 && (variant == 4 || three_launch(B, tp.ntiles));
+    int rc = launch_chain_pp_0(e, a, rgrid, three, s);
+    if (rc == kNotFused) rc = launch_chain_pp_1(e, a, rgrid, three, s);
+    if (rc == kNotFused) rc = launch_chain_pp_2(e, a, rgrid, three, s);
+    if (rc == kNotFused) rc = launch_chain_pp_3(e, a, rgrid, three, s);
     if (rc == kNotFused) return set_error(DSP_EINVAL, "no per-phase kernel for entry %d", tp.pp);
     return rc;
   } else if (tp.kind == 1) {

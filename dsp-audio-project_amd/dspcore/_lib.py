@@ -73,6 +73,7 @@ _SIGNATURES = {
     "dsp_chain_spin_limit": (_c_i64, [_c_i64]),
     "dsp_chain_path": (ctypes.c_int, [_c_i32]),
     "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
+    "dsp_chain_mode": (_c_i32, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,
                                           _c_i64, _c_i32, _c_i64]),
     "dsp_chain_xstate_geometry": (ctypes.c_int, [
@@ -166,8 +167,8 @@ def chain_path(path: int = -1) -> int:
     """Path of dsp_chain_f32 on the calling thread (dsp_chain_path): 0 the
     single-pass kernel where it applies (default), 1 always the two-launch
     chain, 2 / 3 the single-pass path with its chained-tile / persistent
-    kernel (include/dspcore.h); -1 only queries.  Returns the previous
-    setting."""
+    kernel, 4 the three-launch mode of the cascade alone (include/dspcore.h);
+    -1 only queries.  Returns the previous setting."""
     rc = load().dsp_chain_path(int(path))
     if rc < 0:
         check(rc, "dsp_chain_path")

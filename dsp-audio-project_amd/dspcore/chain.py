@@ -96,6 +96,11 @@ class Chain:
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
         # the row into far fewer chunks than the plain rule.
         mc = max_chunks_for(self.B if plan_batch is None else int(plan_batch))
+        # a shard of a job runs the single-pass mode the job's batch takes
+        # (ops.forced_chain_path; the modes agree to float64 rounding only)
+        self._force = ops.forced_chain_path(
+            None if plan_batch is None or int(plan_batch) == self.B else int(plan_batch),
+            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S)
         plain = chunk_len_for(n_out, mc)
         eligible = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
                     and 1 <= S <= 8 and S != 7)
@@ -254,7 +259,7 @@ class Chain:
         S = self.sos.shape[0]
         clip = 0 if self.eq.bypass else 1
         y_ptr = self.y.data_ptr() if self.y is not None else None
-        with torch.cuda.device(self.device):
+        with torch.cuda.device(self.device), self._force:
             stream = torch.cuda.current_stream(self.device)
             rc = lib.dsp_chain_f32(
                 x.data_ptr(), y_ptr, self.z.data_ptr(), self.mag.data_ptr(),

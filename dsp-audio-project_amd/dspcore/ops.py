@@ -186,6 +186,103 @@ def biquad_cascade(x: torch.Tensor, sos: np.ndarray, clip: bool,
     return out
 
 
+_ONE_TAP = SrcPlan(1, 1, 1, np.ones(1), 0, 0, 0, 0)
+
+
+def _eq_tile_plan(n: int, sos: np.ndarray, device: torch.device):
+    """(device tables, key, one-tap taps) of the single-pass cascade alone for
+    rows of n samples (dsp_chain_tile_tables for the SRC bypass as the one-tap
+    SRC, include/dspcore.h), cached; None where no single-pass kernel serves
+    it (n % 4, S outside 1..6, a b0 == 0 band, shared poles)."""
+    import ctypes
+    S = sos.shape[0]
+    lib = _lib.load()
+    if not 1 <= S <= 6 or lib.dsp_chain_tile_len(n, n, 1, 1, 1, 0, S) <= 0:
+        return None
+
+    def build():
+        nbytes = int(lib.dsp_chain_tile_tables_bytes())
+        host = np.zeros(nbytes, dtype=np.uint8)
+        one = np.ones(1, dtype=np.float32)
+        key = ctypes.c_uint64(0)
+        rc = lib.dsp_chain_tile_tables(host.ctypes.data, nbytes, n, n, one.ctypes.data, 1, 1, 1,
+                                       0, _lib.sos_pointer(sos), S, ctypes.byref(key))
+        if rc < 0:
+            _lib.check(rc, "dsp_chain_tile_tables")
+        if rc != 0:
+            return ()
+        return (torch.from_numpy(host).to(device), int(key.value),
+                torch.ones(1, dtype=torch.float32, device=device))
+    plan = _cached(("EQT", sos.tobytes(), n, device.index), build)
+    return plan or None
+
+
+class forced_chain_path:
+    """Sets dsp_chain_path on the calling thread to the path the default would
+    take for a batch of plan_batch rows (dsp_chain_mode: 2 chained tiles, 4 the
+    three-launch mode), unless a path is already forced; restores it after.
+    Shards of one job use it so that every shard's rows are bitwise the
+    unsharded call's (the two modes agree to float64 rounding only)."""
+
+    def __init__(self, plan_batch: int | None, n_in: int, n_out: int, K: int, L: int, M: int,
+                 c: int, S: int):
+        self.path = None
+        if plan_batch is not None:
+            mode = _lib.load().dsp_chain_mode(int(plan_batch), n_in, n_out, K, L, M, c, S)
+            self.path = 4 if mode == 3 else 2 if mode == 1 else None
+
+    def __enter__(self):
+        self.prev = None
+        if self.path is not None and _lib.chain_path() == 0:
+            self.prev = _lib.chain_path(self.path)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            _lib.chain_path(self.prev)
+
+
+def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = None,
+                   plan_batch: int | None = None) -> torch.Tensor | None:
+    """z = clip(cascade(x)) per row (dsp_core.py:233-254) through the
+    single-pass kernel of the cascade alone: dsp_chain_f32 with the SRC bypass
+    as the one-tap SRC (L = M = 1, K = 1, tap 1.0), y = NULL, mag = NULL -- x
+    read once, z written once; small batches of long rows take its
+    three-launch mode (the library picks it, for plan_batch rows when given:
+    forced_chain_path).  Returns None where that kernel does not serve the
+    call (biquad_cascade does)."""
+    x = _rows(x, "x")
+    if x.dtype != torch.float32:
+        x = x.float()
+    sos = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 5)
+    B, n = x.shape
+    if B == 0 or ld(x) % 4 or x.data_ptr() % 16:
+        return None
+    plan = _eq_tile_plan(n, sos, x.device)
+    if plan is None:
+        return None
+    tables, key, taps = plan
+    if out is None:
+        out = torch.empty((B, n), dtype=torch.float32, device=x.device)
+    if ld(out) % 4 or out.data_ptr() % 16 or out.stride(1) != 1:
+        return None
+    lib = _lib.load()
+    S = sos.shape[0]
+    chunk = chunk_len_for(n, max_chunks_for(B))
+    ws_bytes = int(lib.dsp_chain_workspace_bytes(B, n, n, 1, 1, 1, 0, S, chunk))
+    # zero-filled: the chained tiles' hand-off flags start clear (a completed
+    # call leaves them clear; the cached allocator's block is not assumed so)
+    ws = torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device)
+    force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S)
+    with torch.cuda.device(x.device), force:
+        rc = lib.dsp_chain_f32(
+            _ptr(x), None, _ptr(out), None, B, n, ld(x), n, ld(out), _ptr(taps), 1, 1, 1, 0,
+            _lib.sos_pointer(sos), S, 1, chunk, None, None, 0, _ptr(tables), key, 0, 0, 0, 0,
+            None, None, _ptr(ws), ws.numel(), _stream(x.device))
+    _lib.check(rc, "dsp_chain_f32")
+    return out
+
+
 def lfilter_nonfinite(x: torch.Tensor, y: torch.Tensor, b: np.ndarray, a: np.ndarray) -> torch.Tensor:
     """Gives y = lfilter(b, a, x) (len(a) >= 2), computed by the cascade kernel,
     scipy's inf / NaN labels from x's first non-finite sample on

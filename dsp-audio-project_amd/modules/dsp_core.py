@@ -318,7 +318,12 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
 
 
 def sistema_ecualizador(x_n, fs, ganancias_bandas):
-    """6-band peaking-EQ cascade + clip to [-1, 1] (dsp_core.py:216-254)."""
+    """6-band peaking-EQ cascade + clip to [-1, 1] (dsp_core.py:216-254).
+
+    Rows of a multiple of 4 samples run the single-pass kernel of the cascade
+    alone (ops.eq_single_pass: x read once, z written once; a single long
+    channel, as app.py:167 passes, takes its three-launch mode instead of
+    chained tiles); other rows the two-pass cascade (ops.biquad_cascade)."""
     plan = _design.eq_plan(fs, ganancias_bandas)
     if plan.bypass:
         return x_n
@@ -328,4 +333,11 @@ def sistema_ecualizador(x_n, fs, ganancias_bandas):
     else:  # no stage applied: np.clip of x_n.copy() keeps a floating dtype
         dt = np.asarray(x_n).dtype if not _is_tensor(x_n) else np.float32
         out_dtype = dt if np.issubdtype(dt, np.floating) else np.float64
-    return _run(x_n, lambda t, B: _cascade(ops, t, plan.sos, True, B), out_dtype)
+
+    def run(t, B):
+        # the single-pass cascade alone where it serves the rows (x read once,
+        # z written once; one long channel takes its three-launch mode), else
+        # the two-pass cascade
+        z = ops.eq_single_pass(t, plan.sos, plan_batch=B) if plan.sos.shape[0] else None
+        return z if z is not None else _cascade(ops, t, plan.sos, True, B)
+    return _run(x_n, run, out_dtype)

@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 31
+    assert len(names) == 32
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -151,7 +151,7 @@ def test_wav_header_matches_scipy_writer():
 
 
 def test_chain_path_tile_len_and_workspace_query():
-    """dsp_chain_path takes 0..3 (-1 queries); dsp_chain_tile_len names the
+    """dsp_chain_path takes 0..4 (-1 queries); dsp_chain_tile_len names the
     single-pass geometries (config 3's L3/M2, K = 121: 48-sample sub-chunks;
     any L/M with ceil(K/L) <= 8, e.g. config 5's 160/147, K = 1023: 32) and
     declines others; the chain workspace holds a 256-byte status header, the
@@ -159,8 +159,8 @@ def test_chain_path_tile_len_and_workspace_query():
     tiles) and, after it, the two-launch cascade's scratch (never shared)."""
     lib = _lib.load()
     prev = lib.dsp_chain_path(-1)
-    assert prev in (0, 1, 2, 3)
-    assert lib.dsp_chain_path(4) == _lib.DSP_EINVAL
+    assert prev in (0, 1, 2, 3, 4)
+    assert lib.dsp_chain_path(5) == _lib.DSP_EINVAL
     assert lib.dsp_chain_path(-2) == _lib.DSP_EINVAL
     assert lib.dsp_chain_path(-1) == prev
     assert lib.dsp_chain_tile_len(48000, 72000, 121, 3, 2, 60, 6) == 48

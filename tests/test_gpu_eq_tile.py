@@ -165,3 +165,118 @@ def test_cascade_alone_unaligned_rows_take_two_pass(gpu):
     assert "chain_tile" not in names, names
     (_, z0, _), _ = _traced(lambda: ch.run(x.contiguous()))
     assert (z1 - z0).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("B,n_in", [(1, 441000), (3, 441000), (5, 48000), (2, 3072), (4, 96),
+                                    (2, 882000)])
+def test_three_launch_mode_matches_chained(gpu, B, n_in):
+    """The three-launch mode of the cascade alone (dsp_chain_path 4, chain_tile.h
+    AggEntry / GivenEntry, k_tile_carry): every tile from a zero state, the
+    channel's tile states scanned, every tile again from its entry state.
+    Against the chained tiles (path 2) on the same batch: z within 2e-6 (the
+    carries sum in another order), |X| within 1e-5; rows against the oracle;
+    the default takes it for small batches of long rows (one 441000-sample
+    channel: 144 tiles) and leaves the hand-off flags clear."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    n_fft = 4096 if n_in >= 3000 else 128
+    cfg = ChainConfig(n_in, 44100, 1, 1, None, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu, keep_y=False)
+    gen = torch.Generator(device=gpu).manual_seed(B * 7 + n_in % 97)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0] *= 8.0
+    with _chain_path(4):
+        (_, z4, m4), names4 = _traced(lambda: ch.run(x))
+    with _chain_path(2):
+        (_, z2, m2), names2 = _traced(lambda: ch.run(x))
+    (_, z0, m0), names0 = _traced(lambda: ch.run(x))
+    assert "chain_tile_agg" in names4 and "chain_tile_carry" in names4, names4
+    assert "chain_tile_agg" not in names2, names2
+    ntiles = -(-n_in // (64 * 48))
+    if B <= 3 and ntiles >= 16:
+        assert "chain_tile_agg" in names0, names0        # the default's pick
+    assert ch.handoff_ok()
+    assert (z4 - z2).abs().max().item() <= 2e-6
+    assert (m4 - m2).abs().max().item() <= MAG_RTOL * m2.abs().max().item()
+    z = z4.cpu().numpy()
+    for b in (0, B - 1):
+        _, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 44100, 1, 1, orc.CONFIG3_GAINS, None,
+                                      n_fft)
+        assert np.max(np.abs(z[b] - rz)) <= EQ_ATOL
+        assert np.max(np.abs(m4[b].cpu().numpy() - rmag)) <= MAG_RTOL * np.max(rmag)
+
+
+def test_three_launch_mode_nonfinite(gpu):
+    """Non-finite input through the three-launch mode: the repair kernel reruns
+    the channels from their first non-finite tile state (launch 3 published
+    the end states), masks equal to the two-pass cascade's."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 3, 96000
+    cfg = ChainConfig(n_in, 48000, 1, 1, None, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, B, gpu)
+    gen = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0, 40000] = float("nan")
+    x[1, 3072 * 7] = float("inf")
+    x[2, n_in - 2] = float("-inf")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with _chain_path(4):
+            (_, z4, _), names = _traced(lambda: ch.run(x))
+        (_, z0, _), _ = _traced(lambda: ch.run_stages(x))
+    assert "chain_tile_agg" in names and "chain_repair" in names, names
+    a, b = z4.cpu().numpy(), z0.cpu().numpy()
+    for f in (np.isnan, np.isposinf, np.isneginf):
+        np.testing.assert_array_equal(f(a), f(b))
+    fin = np.isfinite(b)
+    assert np.max(np.abs(a[fin] - b[fin])) <= 2e-6
+    assert ch.handoff_ok()
+
+
+def test_drop_in_equaliser_one_long_channel(gpu):
+    """sistema_ecualizador on one 441000-sample channel, as app.py:167 calls it
+    after the 2/1 SRC (882000 samples) and at L = M = 1: the single-pass cascade
+    alone in its three-launch mode (traced), float64 out, within 1e-5 of the
+    oracle (dsp_core.py:216-254) and of the two-pass cascade."""
+    from dspcore import _lib
+    from oracle import dsp_ref_cpu as orc
+    import modules.dsp_core as dc
+    rng = np.random.default_rng(12)
+    for n in (441000, 882000):
+        x = rng.uniform(-1, 1, n).astype(np.float64) * 0.8
+        _lib.trace_enable(True)
+        _lib.trace_read()
+        try:
+            z = dc.sistema_ecualizador(x, 44100 if n == 441000 else 88200, orc.CONFIG3_GAINS)
+            names = [nm for nm, _ in _lib.trace_read()]
+        finally:
+            _lib.trace_enable(False)
+        assert "chain_tile_agg" in names and "chain_tile_carry" in names, names
+        assert not any(nm.startswith("iir") for nm in names), names
+        assert z.dtype == np.float64 and z.shape == (n,)
+        rz = orc.equaliser(x, 44100 if n == 441000 else 88200, orc.CONFIG3_GAINS)
+        assert np.max(np.abs(z - rz)) <= EQ_ATOL
+
+
+def test_drop_in_equaliser_shards_take_the_jobs_mode(gpu, monkeypatch):
+    """A sharded drop-in batch runs, on every shard, the single-pass mode the
+    whole batch takes (dsp_chain_mode, ops.forced_chain_path): 400 rows of
+    48000 samples take chained tiles whole, while a 100-row shard alone would
+    take the three-launch mode; the four-shard rows are bitwise the one-device
+    rows."""
+    from dspcore import _lib
+    from oracle import dsp_ref_cpu as orc
+    import modules.dsp_core as dc
+    lib = _lib.load()
+    assert lib.dsp_chain_mode(400, 48000, 48000, 1, 1, 1, 0, 6) == 1
+    assert lib.dsp_chain_mode(100, 48000, 48000, 1, 1, 1, 0, 6) == 3
+    assert lib.dsp_chain_mode(1, 48000, 48000, 41, 1, 1, 20, 6) == 0
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-0.9, 0.9, (400, 48000)).astype(np.float32)
+    monkeypatch.setattr(dc, "_shard_devices", lambda: [gpu])
+    one = dc.sistema_ecualizador(x, 48000, orc.CONFIG3_GAINS)
+    monkeypatch.setattr(dc, "_shard_devices", lambda: [gpu] * 4)
+    four = dc.sistema_ecualizador(x, 48000, orc.CONFIG3_GAINS)
+    np.testing.assert_array_equal(one, four)
+    assert _lib.chain_path() == 0            # restored

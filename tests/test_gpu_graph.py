@@ -16,7 +16,8 @@ Geometries: config 3 at full size (k_chain_tile, 4096 channels x 24 tiles:
 many dispatch generations), config 5 at full size (the persistent
 k_chain_gcp<160, 147>), the config-4 kernel at 16384 channels, two of the
 app's ratios on the per-phase kernels (2/1 and 3/4, 4096 channels) and the
-app's default 1/1 (the cascade alone, 4096 channels).
+app's default 1/1 (the cascade alone: chained tiles at 4096 channels, the
+three-launch mode at 2).
 """
 import numpy as np
 import pytest
@@ -60,6 +61,8 @@ def _workspace_clear(ch):
     ("ratio-3/4", 4096, 48000, 3, 4, None, (0, 4095)),
     # the SRC bypass: the cascade alone (one-tap SRC, y is x)
     ("eq-only", 4096, 48000, 1, 1, None, (0, 4095)),
+    # ... and at 2 channels, where it takes the three-launch mode
+    ("eq-only-b2", 2, 48000, 1, 1, None, (0, 1)),
 ])
 def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
     from dspcore.chain import Chain, ChainConfig
@@ -74,7 +77,7 @@ def test_graph_replay_matches_eager(gpu, tag, B, fs, L, M, K, kernel_rows):
         x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
         # a clipped row, a different one per replay (x 8 at the app's ratios:
         # tests/test_gpu_pp.py says why)
-        x[r] *= 8.0 if tag.startswith("ratio") else 40.0
+        x[r % B] *= 8.0 if tag.startswith("ratio") else 40.0
         xs.append(x)
     # eager reference runs (hand-off status checked after each)
     eager = []
