@@ -521,7 +521,8 @@ def app_rerun(device, reps=5):
     (conversion_tasa_muestreo then sistema_ecualizador) and the three spectra
     of :203-205 (x, y and z, each on its first 100000 samples) -- on a
     441000-sample channel (10 s at 44.1 kHz, the config-1 stand-in for the
-    missing FastCar.wav) with the config-3 gains, at L/M 2/1 and 3/2.  numpy in,
+    missing FastCar.wav) with the config-3 gains, at L/M 1/1 (the sliders'
+    default: the SRC returns x, the EQ is the whole path), 2/1 and 3/2.  numpy in,
     numpy out, as app.py calls it; ms per rerun (median of `reps` after one
     warm) next to the oracle (oracle/dsp_ref_cpu.py, the reference's numpy /
     scipy calls) on the same host and input, one process.  Not the metric."""
@@ -559,7 +560,7 @@ def app_rerun(device, reps=5):
 
     out = {}
     with torch.cuda.device(device):
-        for L, M in ((2, 1), (3, 2)):
+        for L, M in ((1, 1), (2, 1), (3, 2)):   # (1/1: the sliders' default, app.py:149-150)
             g = median_ms(lambda: rerun_gpu(L, M), reps)
             c = median_ms(lambda: rerun_cpu(L, M), 3)
             got, ref = rerun_gpu(L, M), rerun_cpu(L, M)
@@ -627,6 +628,8 @@ def ratio_sweep(device, channels=4096, steps=8, cases=None, two_launch=True):
         rate = lambda v: round(channels * 48000 / (v * 1e-3) / 1e6, 1)  # noqa: E731
         rows.append({"L": L, "M": M, "K": ch.src.K, "path": "single-pass" if single else
                      ("eq-only (SRC identity)" if ch.identity_src else "two-launch"),
+                     **({"note": "SRC bypass: the cascade alone (one-tap single-pass)"}
+                        if ch.identity_src and single else {}),
                      "tile_len": ch.tile_len, "ms": round(ms, 4), "msamples_s": rate(ms),
                      **({"two_launch_ms": round(ms2, 4), "two_launch_msamples_s": rate(ms2),
                          "speedup_vs_two_launch": round(ms2 / ms, 3)} if ms2 else {}),
