@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   chain_pp_body<G, false>(a, lds, threadIdx.x, blockIdx.x, blockIdx.y);
 }
 
-// Launches 1 and 3 of the three-launch mode (the cascade alone).
+// Launches 1 and 3 of the three-launch mode (chain_tile.h, AggEntry).
 template <class G, int MODE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_pp3(
     TileArgs a) {
@@ -334,24 +334,21 @@ struct PpEntry {
 // states[] scanned into the tiles' entry states, per channel.
 void launch_tile_carry(const TileArgs& a, int tile_len, hipStream_t s);
 
-// Launches k_chain_pp<G> (three: the three-launch mode, built for the cascade
-// alone) and its repair kernel on s (the caller checked the geometry, tables
+// Launches k_chain_pp<G> (three: the three-launch mode instead) and its
+// repair kernel on s (the caller checked the geometry, tables
 // and workspace: chain_tile.hip launch_chain_tile).
 template <class G>
 int pp_launch(const TileArgs& a, unsigned rgrid, bool three, hipStream_t s) {
   const dim3 grid((unsigned)a.B, (unsigned)a.ntiles);
-  if constexpr (G::IDENT) {
-    if (three) {
-      {
-        TraceScope trace("chain_tile_agg", s);
-        hipLaunchKernelGGL((k_chain_pp3<G, 1>), grid, dim3(kWave), 0, s, a);
-      }
-      launch_tile_carry(a, G::TS, s);
-      TraceScope trace("chain_tile", s);
-      hipLaunchKernelGGL((k_chain_pp3<G, 2>), grid, dim3(kWave), 0, s, a);
+  if (three) {
+    {
+      TraceScope trace("chain_tile_agg", s);
+      hipLaunchKernelGGL((k_chain_pp3<G, 1>), grid, dim3(kWave), 0, s, a);
     }
-  }
-  if (!G::IDENT || !three) {
+    launch_tile_carry(a, G::TS, s);
+    TraceScope trace("chain_tile", s);
+    hipLaunchKernelGGL((k_chain_pp3<G, 2>), grid, dim3(kWave), 0, s, a);
+  } else {
     TraceScope trace("chain_tile", s);
     hipLaunchKernelGGL(k_chain_pp<G>, grid, dim3(kWave), 0, s, a);
   }

@@ -93,7 +93,9 @@ namespace dsp {
 namespace {
 
 // One tile of the L3/M2 kernel (REPAIR: the rerun with the non-finite path).
-template <class GEO, bool DLY, bool REPAIR>
+// MODE: 0 the chained hand-off, 1 / 2 launch 1 / 3 of the three-launch mode
+// (chain_tile.h, AggEntry / GivenEntry).
+template <class GEO, bool DLY, bool REPAIR, int MODE = 0>
 __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, int lane, int64_t b,
                                                 int64_t tile) {
   constexpr int TS = GEO::TSUB;
@@ -107,7 +109,8 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
   // requires -- and arrives behind the SRC and pass 1 instead of two global
   // round trips after them.  Otherwise tile_cascade waits as before.
   uint32_t fl = 0;
-  if (!REPAIR && tile > 0 && lane == 0) fl = load_flag(a.flags + b * a.ntiles + tile - 1);
+  if (!REPAIR && MODE == 0 && tile > 0 && lane == 0)
+    fl = load_flag(a.flags + b * a.ntiles + tile - 1);
 
   // ---- x window of the tile -> padded LDS image (x == 0 outside [0, n_in))
   {
@@ -132,7 +135,7 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
   }
   fence();  // one wave: its LDS operations execute in order
   EarlyEntry early{false, reinterpret_cast<const double*>(lds + GEO::LDSF)};
-  if (!REPAIR && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
+  if (!REPAIR && MODE == 0 && tile > 0 && __builtin_amdgcn_readfirstlane(fl) == 1u) {
     early.early = true;
     if (lane < 2 * kD) {
       const int64_t prev = b * a.ntiles + tile - 1;
@@ -173,6 +176,10 @@ __device__ __forceinline__ void chain_tile_body(const TileArgs& a, float* lds, i
       });
     };
     tile_cascade<TS, true, true>(a, mt, lds, y, lane, b, tile, m0, fix);
+  } else if constexpr (MODE == 1) {
+    tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0, AggEntry{});
+  } else if constexpr (MODE == 2) {
+    tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0, GivenEntry{});
   } else {
     tile_cascade<TS>(a, mt, lds, y, lane, b, tile, m0, 0, early);
   }
@@ -185,6 +192,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   // grid (B, ntiles): linear ids tile-major (x fastest), no division
   const int64_t tile = blockIdx.y, b = blockIdx.x;
   chain_tile_body<GEO, DLY, false>(a, lds, threadIdx.x, b, tile);
+}
+
+// Launches 1 and 3 of the three-launch mode (chain_tile.h, AggEntry).
+template <class GEO, bool DLY, int MODE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_chain_tile3(
+    TileArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[GEO::LDSF];
+  chain_tile_body<GEO, DLY, false, MODE>(a, lds, threadIdx.x, blockIdx.x, blockIdx.y);
 }
 
 template <class GEO, bool DLY = false>
@@ -1281,16 +1296,20 @@ __global__ __launch_bounds__(kWave * kS) void k_tile_carry(TileArgs a) {
   }
 }
 
-// Whether the cascade alone takes the three-launch mode: when the chained
+// Whether a single-pass launch takes the three-launch mode: when the chained
 // hand-off (~2.2 us a tile: one 441000-sample channel, 144 tiles, 0.31 ms)
-// would bound the launch.  Fitted to both modes forced on one box at 1..4096
-// channels of 48000 and 441000 samples (profiles/r06_eq_alone_modes.txt):
-// chained ~ 2.2 us ntiles + 5 ns B ntiles, three launches ~ 15 us + 8.4 ns
-// B ntiles (each tile's x, pass 1 and scan twice; two more launches).
-bool three_launch(int64_t B, int64_t ntiles) {
+// would bound it.  With t the tile's throughput cost at a full chip, chained
+// ~ 2.2 us ntiles + 0.8 t B ntiles and three launches ~ 15 us + 1.4 t B
+// ntiles (launch 1 redoes each tile's x, SRC, pass 1 and scan: ~0.4 t; two
+// more launches).  Fitted on the cascade alone (t = 6 ns; both modes forced
+// on one box at 1..4096 channels of 48000 and 441000 samples,
+// profiles/r06_eq_alone_modes.txt) and checked on the SRC kernels (t = 7 ns,
+// profiles/r06_three_launch_modes.txt).
+bool three_launch(int64_t B, int64_t ntiles, double t_tile) {
   const double tiles = (double)B * (double)ntiles;
-  return 15e-6 + 8.4e-9 * tiles < 2.2e-6 * (double)ntiles + 5e-9 * tiles;
+  return 15e-6 + 1.4 * t_tile * tiles < 2.2e-6 * (double)ntiles + 0.8 * t_tile * tiles;
 }
+constexpr double kTileCostIdent = 6e-9, kTileCostSrc = 7e-9;
 
 }  // namespace
 
@@ -1309,8 +1328,10 @@ int chain_mode(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M, int6
   if (B < 1 || !tile_geometry(n_in, n_out, K, L, M, c, S, &tp)) return 0;
   if (tp.kind == 4) {
     const PpEntry& e = kPpEntries[tp.pp];
-    if (e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0 && three_launch(B, tp.ntiles)) return 3;
+    const bool ident = e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0;
+    if (three_launch(B, tp.ntiles, ident ? kTileCostIdent : kTileCostSrc)) return 3;
   }
+  if (tp.kind == 1 && three_launch(B, tp.ntiles, kTileCostSrc)) return 3;
   return 1;
 }
 
@@ -1446,10 +1467,11 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     const PpNeed n = pp_need(K, L, M, c);
     a.cq = n.xa0;
     const PpEntry& e = kPpEntries[tp.pp];
-    // the cascade alone (the one-tap SRC bypass): the three-launch mode for
-    // small batches of long rows (variant 4 forces it, 2 the chained tiles)
+    // the three-launch mode for small batches of long rows (variant 4 forces
+    // it, 2 the chained tiles)
     const bool ident = e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0;
-    const bool three = ident && variant != 2 && (variant == 4 || three_launch(B, tp.ntiles));
+    const bool three = variant != 2 &&
+        (variant == 4 || three_launch(B, tp.ntiles, ident ? kTileCostIdent : kTileCostSrc));
     int rc = launch_chain_pp_0(e, a, rgrid, three, s);
     if (rc == kNotFused) rc = launch_chain_pp_1(e, a, rgrid, three, s);
     if (rc == kNotFused) rc = launch_chain_pp_2(e, a, rgrid, three, s);
@@ -1459,10 +1481,21 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   } else if (tp.kind == 1) {
     // (No persistent variant: one measured 9 % slower at config 4 and 5 % at
     // config 3 than these chained tiles, profiles/r04_tilep_ab.txt.)
-    {
+    const dim3 grid((unsigned)B, (unsigned)tp.ntiles);
+    if (variant != 2 && (variant == 4 || three_launch(B, tp.ntiles, kTileCostSrc))) {
+      {
+        TraceScope trace("chain_tile_agg", s);
+        auto k1 = dly ? k_chain_tile3<Geo3241, true, 1> : k_chain_tile3<Geo3241, false, 1>;
+        hipLaunchKernelGGL(k1, grid, dim3(kWave), 0, s, a);
+      }
+      launch_tile_carry(a, Geo3241::TSUB, s);
+      TraceScope trace("chain_tile", s);
+      auto k3 = dly ? k_chain_tile3<Geo3241, true, 2> : k_chain_tile3<Geo3241, false, 2>;
+      hipLaunchKernelGGL(k3, grid, dim3(kWave), 0, s, a);
+    } else {
       TraceScope trace("chain_tile", s);
       auto kern = dly ? k_chain_tile<Geo3241, true> : k_chain_tile<Geo3241, false>;
-      hipLaunchKernelGGL(kern, dim3((unsigned)B, (unsigned)tp.ntiles), dim3(kWave), 0, s, a);
+      hipLaunchKernelGGL(kern, grid, dim3(kWave), 0, s, a);
     }
     TraceScope trace("chain_repair", s);
     auto rep = dly ? k_chain_tile_repair<Geo3241, true> : k_chain_tile_repair<Geo3241, false>;

@@ -280,3 +280,67 @@ def test_drop_in_equaliser_shards_take_the_jobs_mode(gpu, monkeypatch):
     four = dc.sistema_ecualizador(x, 48000, orc.CONFIG3_GAINS)
     np.testing.assert_array_equal(one, four)
     assert _lib.chain_path() == 0            # restored
+
+
+@pytest.mark.parametrize("L,M,B,n_in", [(2, 1, 1, 441000), (3, 2, 2, 96000), (1, 2, 2, 441000),
+                                        (3, 4, 3, 96000), (5, 4, 1, 48000), (8, 8, 2, 96000)])
+def test_three_launch_mode_src_ratios(gpu, L, M, B, n_in):
+    """The three-launch mode on the SRC kernels (k_chain_tile3 for 3/2,
+    k_chain_pp3 for the per-phase ratios): against the chained tiles (path 2)
+    y bitwise (one SRC), z within 2e-6, |X| within 1e-5; rows against the
+    oracle; the default takes it for one or two long channels."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    cfg = ChainConfig(n_in, 48000, L, M, None, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len > 0
+    gen = torch.Generator(device=gpu).manual_seed(L * 9 + M + B)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0] *= 8.0
+    with _chain_path(4):
+        (y4, z4, m4), names4 = _traced(lambda: ch.run(x))
+    with _chain_path(2):
+        (y2, z2, m2), names2 = _traced(lambda: ch.run(x))
+    (_, _, _), names0 = _traced(lambda: ch.run(x))
+    assert "chain_tile_agg" in names4 and "chain_tile_carry" in names4, names4
+    assert "chain_tile_agg" not in names2, names2
+    if n_in * L // M >= 96000 * 2:
+        assert "chain_tile_agg" in names0, names0
+    assert ch.handoff_ok()
+    assert torch.equal(y4, y2)
+    assert (z4 - z2).abs().max().item() <= 2e-6
+    assert (m4 - m2).abs().max().item() <= MAG_RTOL * m2.abs().max().item()
+    for b in range(B):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, L, M, orc.CONFIG3_GAINS, None,
+                                       2048)
+        assert np.max(np.abs(y4[b].cpu().numpy() - ry)) <= 2e-6 * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z4[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(m4[b].cpu().numpy() - rmag)) <= MAG_RTOL * np.max(rmag)
+
+
+@pytest.mark.parametrize("L,M", [(3, 2), (2, 1)])
+def test_three_launch_mode_src_nonfinite(gpu, L, M):
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 3, 48000
+    cfg = ChainConfig(n_in, 48000, L, M, None, orc.CONFIG3_GAINS, n_fft=2048)
+    ch = Chain(cfg, B, gpu)
+    gen = torch.Generator(device=gpu).manual_seed(8)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0, 20000] = float("nan")
+    x[1, 4096] = float("inf")
+    x[2, n_in - 1] = float("-inf")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with _chain_path(4):
+            (y4, z4, _), names = _traced(lambda: ch.run(x))
+        with _chain_path(1):
+            (y0, z0, _), _ = _traced(lambda: ch.run(x))
+    assert "chain_tile_agg" in names and "chain_repair" in names, names
+    for a, b, tol in ((y4, y0, 0.0), (z4, z0, 2e-6)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        for f in (np.isnan, np.isposinf, np.isneginf):
+            np.testing.assert_array_equal(f(a), f(b))
+        fin = np.isfinite(b)
+        assert np.max(np.abs(a[fin] - b[fin])) <= tol
+    assert ch.handoff_ok()

@@ -1,4 +1,5 @@
-"""The cascade alone (L = M = 1, config-3 gains): the single-pass one-tap
+"""The cascade alone (L = M = 1, config-3 gains; --ratio L/M for another
+ratio, y not kept): the single-pass one-tap
 kernel (Chain.run) against the two-pass cascade (Chain.run_stages) on the same
 box, HIP-graph replay like bench.py, for the batch shapes given as BxN
 (default 4096x48000 32768x48000 1x441000 1x48000 16x441000).  Prints ms per
@@ -44,11 +45,18 @@ def graph_ms(fn, reps):
 
 
 def main():
-    shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]] or \
+    args = sys.argv[1:]
+    L = M = 1
+    if "--ratio" in args:   # another SRC ratio through the same three paths
+        i = args.index("--ratio")
+        L, M = (int(v) for v in args[i + 1].split("/"))
+        del args[i:i + 2]
+    shapes = [tuple(int(v) for v in a.split("x")) for a in args] or \
         [(4096, 48000), (32768, 48000), (1, 441000), (1, 48000), (16, 441000)]
     dev = torch.device("cuda", 0)
+    print(f"L/M {L}/{M}", flush=True)
     for B, n in shapes:
-        cfg = ChainConfig(n, 48000, 1, 1, None, GAINS, n_fft=4096)
+        cfg = ChainConfig(n, 48000, L, M, None, GAINS, n_fft=4096)
         ch = Chain(cfg, B, dev, keep_y=False)
         x = torch.rand((B, n), device=dev) * 2 - 1
         reps = max(5, min(200, int(2e9 // (B * n * 8))))
@@ -62,7 +70,7 @@ def main():
             finally:
                 _lib.chain_path(prev)
         ch.check()
-        gbs = B * n * 8 / (t1 * 1e-3) / 1e9
+        gbs = B * (n * 4 + ch.n_out * 4) / (t1 * 1e-3) / 1e9
         print(f"B={B} n={n}: single-pass {t1:.4f} ms ({gbs:.0f} GB/s x+z, "
               f"{B * n / t1 / 1e6:.1f} G samples/s), two-pass {t0:.4f} ms, x{t0 / t1:.2f} "
               f"(tile_len {ch.tile_len}); chained {paths[2]:.4f} ms, three-launch "
