@@ -216,7 +216,11 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * whichever path served it: its first 256 bytes are a status header (word 0),
  * followed by the single-pass kernel's hand-off region, followed by the
  * two-launch cascade's scratch; the two paths never share bytes.  Each row's
- * result is bitwise independent of B.
+ * result is bitwise independent of B for a given path and mode: y always;
+ * z and mag across the default's choice of the single-pass mode (chained
+ * tiles, or from ABI 2.7 the three-launch mode for small batches of long
+ * rows) to float64 rounding only -- dsp_chain_mode(B, ...) names the mode, and
+ * dsp_chain_path 2 / 4 fix it, for callers that split one batch over calls.
  *
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
  * 1 <= S <= 6 with every b0 != 0 (ABI 2.6: S = 0, the EQ bypassed, takes the

@@ -94,8 +94,8 @@ def test_config1_chain_two_launch_bypass(gpu):
     then the S = 0 cascade launch (the bypass copy, no clip: z == y bitwise)
     then the spectrum; with the config-3 gains the same geometry (2/1, K =
     127: 64 taps per branch) takes the per-phase single-pass kernel (csrc/
-    chain_pp.h), whose y is bitwise the two-launch chain's; against the
-    oracle."""
+    chain_pp.h; for two channels this long, its three-launch mode), whose y
+    is bitwise the two-launch chain's; against the oracle."""
     from dspcore.chain import Chain, ChainConfig
     from oracle import dsp_ref_cpu as orc
     x, fs = _fastcar_stand_in()
@@ -112,7 +112,9 @@ def test_config1_chain_two_launch_bypass(gpu):
     ch3 = Chain(cfg3, 2, gpu)
     assert ch3.tile_len == 48
     (y3, _, _), names3 = _traced(lambda: ch3.run(xs))
-    assert names3[:2] == ["chain_tile", "chain_repair"], names3
+    # (two 441000-sample channels: the single-pass kernel's three-launch mode)
+    assert names3[:4] == ["chain_tile_agg", "chain_tile_carry", "chain_tile", "chain_repair"], \
+        names3
     assert torch.equal(y3, y)
     ry, rz, _, rm, _ = orc.chain(x, fs, 2, 1, FLAT, 127, 1024, limit_pts=100000)
     y, mag = y.cpu().numpy(), mag.cpu().numpy()
@@ -177,7 +179,14 @@ def test_handoff_give_up_surfaces_and_reset_recovers(gpu):
     """With a spin limit of 0 (dsp_chain_spin_limit: every wait gives up at its
     first unanswered poll) one channel's tiles, all in flight at once, cannot
     hand off: run() raises HandoffError, and after its reset the workspace
-    serves a normal call bitwise like a fresh chain."""
+    serves a normal call bitwise like a fresh chain.  (The chained tiles
+    forced: one channel alone would take the three-launch mode, which waits
+    for nothing.)"""
+    with _chain_path(2):
+        _handoff_give_up(gpu)
+
+
+def _handoff_give_up(gpu):
     from dspcore import _lib
     from dspcore.chain import Chain, ChainConfig, HandoffError
     from oracle import dsp_ref_cpu as orc

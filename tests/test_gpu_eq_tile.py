@@ -344,3 +344,33 @@ def test_three_launch_mode_src_nonfinite(gpu, L, M):
         fin = np.isfinite(b)
         assert np.max(np.abs(a[fin] - b[fin])) <= tol
     assert ch.handoff_ok()
+
+
+def test_drop_in_host_conversions_match_numpy(gpu):
+    """The drop-in's numpy edges (modules/dsp_core.py _to_rows / _from_rows):
+    float64 and complex128 rows narrowed on the device give numpy astype's
+    float32 / complex64 bits (denormals, halfway cases, inf, NaN included);
+    results come back widened exactly, as float64 / complex128 arrays backed
+    by page-locked memory that stays valid after later calls."""
+    import modules.dsp_core as dc
+    rng = np.random.default_rng(4)
+    a = rng.standard_normal(4099) * np.logspace(-46, 38, 4099)
+    a[:6] = [1e-40, -3e-39, 5e-45, np.inf, -np.inf, np.nan]
+    a[6] = 1.0 + 2.0 ** -24            # halfway: ties to even
+    a[7] = 1.0 + 3 * 2.0 ** -24
+    t, how = dc._to_rows(a)
+    got = t.cpu().numpy()[0]
+    want = a.astype(np.float32)
+    np.testing.assert_array_equal(got.view(np.uint32)[6:], want.view(np.uint32)[6:])
+    np.testing.assert_array_equal(got[:6], want[:6])
+    c = a[:2048] + 1j * a[2048:4096]
+    tc, _ = dc._to_rows(c, complex_ok=True)
+    np.testing.assert_array_equal(tc.cpu().numpy()[0].view(np.uint32)[16:],
+                                  c.astype(np.complex64).view(np.uint32)[16:])
+    back = dc._from_rows(t, how, np.float64)
+    assert back.dtype == np.float64 and back.shape == a.shape
+    np.testing.assert_array_equal(back[6:], want.astype(np.float64)[6:])
+    keep = back.copy()
+    for _ in range(3):                   # later calls do not touch a returned array
+        dc._from_rows(torch.zeros_like(t), how, np.float64)
+    np.testing.assert_array_equal(back, keep)

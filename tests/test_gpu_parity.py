@@ -423,7 +423,9 @@ def test_chain_config3_full_batch(gpu):
     torch.cuda.synchronize()
     assert torch.isfinite(z).all() and torch.isfinite(mag).all()
     assert float(z.abs().max()) <= 1.0
-    one = Chain(cfg, 1, gpu, chunk_len=ch.chunk_len)   # same chunking: bitwise rows
+    # same chunking and single-pass mode (plan_batch: the batch's chained tiles,
+    # not one row's three-launch mode): bitwise rows
+    one = Chain(cfg, 1, gpu, chunk_len=ch.chunk_len, plan_batch=B)
     for b in (0, 1234, B - 1):
         xb = x[b].cpu().numpy()
         ry, rz, _, rmag, _ = orc.chain(xb.astype(np.float32), 48000, 3, 2, orc.CONFIG3_GAINS,
