@@ -293,10 +293,10 @@ __device__ __forceinline__ void gen_fix(const TileArgs& a, tt_ptr mt, const floa
 
 // One tile of k_chain_gen for one wave (REPAIR: the rerun with the
 // non-finite path).
-template <bool UP, bool REPAIR>
+template <bool UP, bool REPAIR, class ENTRY = ChainedEntry>
 __device__ __forceinline__ void chain_gen_body(const TileArgs& a, const float* seq,
                                                const uint32_t* adv, float* win, int lane,
-                                               int64_t b, int64_t tile) {
+                                               int64_t b, int64_t tile, ENTRY&& entry = ENTRY{}) {
   const int L = a.L, M = a.M, T = a.T;
   const tt_ptr mt = (tt_ptr)a.tt;
   const int C = mt->classes;
@@ -376,7 +376,7 @@ __device__ __forceinline__ void chain_gen_body(const TileArgs& a, const float* s
                                        gen_fix(a, mt, win, qa, j0, b, m0 + kGenTS * lane, yy, v);
                                      });
   else
-    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0);
+    tile_cascade<kGenTS>(a, mt, win, y, lane, b, tile, m0, 0, entry);
 }
 
 template <bool UP>
@@ -393,6 +393,24 @@ k_chain_gen(TileArgs a) {
   if (b >= a.B) return;
   float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
   chain_gen_body<UP, false>(a, seq, adv, win, lane, b, tile);
+}
+
+// Launches 1 and 3 of the three-launch mode (chain_tile.h, AggEntry).
+template <bool UP, int MODE>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gen3(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t tile = blockIdx.y;
+  const int64_t b = (int64_t)blockIdx.x * kGenWaves + w;
+  float* seq = smem;
+  uint32_t* adv = reinterpret_cast<uint32_t*>(smem + kGenClasses * kGenClassStride);
+  gen_load_classes(a, seq, adv);
+  if (b >= a.B) return;
+  float* win = smem + kGenClasses * kGenClassStride + kGenClasses + w * a.win;
+  if constexpr (MODE == 1) chain_gen_body<UP, false>(a, seq, adv, win, lane, b, tile, AggEntry{});
+  else chain_gen_body<UP, false>(a, seq, adv, win, lane, b, tile, GivenEntry{});
 }
 
 template <bool UP>
@@ -543,13 +561,14 @@ __device__ __forceinline__ void gct_tile(const TileArgs& a, const float* seq, fl
 }
 
 // One tile of k_chain_gct for one wave: its x window, then gct_tile.
-template <int L, int M, bool T7, bool REPAIR>
+template <int L, int M, bool T7, bool REPAIR, class ENTRY = ChainedEntry>
 __device__ __forceinline__ void chain_gct_body(const TileArgs& a, const float* seq, float* win,
-                                               int lane, int64_t b, int64_t tile) {
+                                               int lane, int64_t b, int64_t tile,
+                                               ENTRY&& entry = ENTRY{}) {
   const int64_t qa = gen_window_start<L, M>(a, tile);
   gen_load_window(a, win, lane, b, qa);
   fence();
-  gct_tile<L, M, T7, REPAIR>(a, seq, win, lane, b, tile, qa);
+  gct_tile<L, M, T7, REPAIR>(a, seq, win, lane, b, tile, qa, entry);
 }
 
 template <int L, int M, bool T7 = false>
@@ -565,6 +584,23 @@ k_chain_gct(TileArgs a) {
   if (b >= a.B) return;
   float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
   chain_gct_body<L, M, T7, false>(a, seq, win, lane, b, tile);
+}
+
+// Launches 1 and 3 of the three-launch mode (chain_tile.h, AggEntry).
+template <int L, int M, bool T7, int MODE>
+__global__ __launch_bounds__(kWave * kGenWaves) __attribute__((amdgpu_waves_per_eu(4))) void
+k_chain_gct3(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = gen_wave();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t tile = blockIdx.y;
+  const int64_t b = (int64_t)blockIdx.x * kGenWaves + w;
+  float* seq = smem;
+  ct_load_classes(a, seq);
+  if (b >= a.B) return;
+  float* win = smem + ((tt_ptr)a.tt)->classes * kCtClassStride + w * a.win;
+  if constexpr (MODE == 1) chain_gct_body<L, M, T7, false>(a, seq, win, lane, b, tile, AggEntry{});
+  else chain_gct_body<L, M, T7, false>(a, seq, win, lane, b, tile, GivenEntry{});
 }
 
 template <int L, int M, bool T7 = false>
@@ -1331,7 +1367,7 @@ int chain_mode(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M, int6
     const bool ident = e.LR == 1 && e.MR == 1 && e.NP == 1 && e.UC == 0;
     if (three_launch(B, tp.ntiles, ident ? kTileCostIdent : kTileCostSrc)) return 3;
   }
-  if (tp.kind == 1 && three_launch(B, tp.ntiles, kTileCostSrc)) return 3;
+  if (tp.kind != 4 && three_launch(B, tp.ntiles, kTileCostSrc)) return 3;
   return 1;
 }
 
@@ -1516,9 +1552,25 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
                              : resident_groups<k_chain_gcp<160, 147, false>>(kWave * kGenWaves, shm);
     const int64_t rounds = res > 0 ? ceil_div(groups, res) : 0;
     const bool fits = tp.win <= 4 * kGcpWin * kWave && tp.win > 4 * (kGcpWin - 1) * kWave;
-    const bool persistent = fits && res > 0 && groups >= res &&
+    // (the three-launch mode is for batches far below the persistent kernel's)
+    const bool three = variant == 4 || (variant == 0 && three_launch(B, tp.ntiles, kTileCostSrc));
+    const bool persistent = !three && fits && res > 0 && groups >= res &&
                             groups * 8 >= rounds * res * 7 && variant != 2;
-    {
+    if (three) {
+      auto k1 = a.T <= 7 ? k_chain_gct3<160, 147, true, 1> : k_chain_gct3<160, 147, false, 1>;
+      auto k3 = a.T <= 7 ? k_chain_gct3<160, 147, true, 2> : k_chain_gct3<160, 147, false, 2>;
+      if (int rc = allow_lds(k1, shm)) return rc;
+      if (int rc = allow_lds(k3, shm)) return rc;
+      {
+        TraceScope trace("chain_tile_agg", s);
+        hipLaunchKernelGGL(k1, dim3((unsigned)groups, (unsigned)tp.ntiles), dim3(kWave * kGenWaves),
+                           shm, s, a);
+      }
+      launch_tile_carry(a, kGenTS, s);
+      TraceScope trace("chain_tile", s);
+      hipLaunchKernelGGL(k3, dim3((unsigned)groups, (unsigned)tp.ntiles), dim3(kWave * kGenWaves),
+                         shm, s, a);
+    } else {
       TraceScope trace("chain_tile", s);
       if (persistent || (variant == 3 && fits))
         hipLaunchKernelGGL(pers, dim3((unsigned)std::min<int64_t>(groups, std::max(res, 1))),
@@ -1536,10 +1588,22 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
     auto rep = M < L ? k_chain_gen_repair<true> : k_chain_gen_repair<false>;
     if (int rc = allow_lds(kern, shm)) return rc;
     if (int rc = allow_lds(rep, shm)) return rc;
-    {
+    const dim3 grid((unsigned)groups, (unsigned)tp.ntiles);
+    if (variant != 2 && (variant == 4 || three_launch(B, tp.ntiles, kTileCostSrc))) {
+      auto k1 = M < L ? k_chain_gen3<true, 1> : k_chain_gen3<false, 1>;
+      auto k3 = M < L ? k_chain_gen3<true, 2> : k_chain_gen3<false, 2>;
+      if (int rc = allow_lds(k1, shm)) return rc;
+      if (int rc = allow_lds(k3, shm)) return rc;
+      {
+        TraceScope trace("chain_tile_agg", s);
+        hipLaunchKernelGGL(k1, grid, dim3(kWave * kGenWaves), shm, s, a);
+      }
+      launch_tile_carry(a, kGenTS, s);
       TraceScope trace("chain_tile", s);
-      hipLaunchKernelGGL(kern, dim3((unsigned)groups, (unsigned)tp.ntiles), dim3(kWave * kGenWaves), shm,
-                         s, a);
+      hipLaunchKernelGGL(k3, grid, dim3(kWave * kGenWaves), shm, s, a);
+    } else {
+      TraceScope trace("chain_tile", s);
+      hipLaunchKernelGGL(kern, grid, dim3(kWave * kGenWaves), shm, s, a);
     }
     TraceScope trace("chain_repair", s);
     hipLaunchKernelGGL(rep, dim3(rgrid), dim3(kWave * kGenWaves), shm, s, a);

@@ -295,7 +295,7 @@ int xstate_geometry(int64_t chunk_len, int K, int L, int M, int64_t c, int64_t* 
 // the instantiated geometry (0: the two-launch chain serves this call).
 int64_t chain_tile_sub(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S);
 // The path dsp_chain_f32's default takes for a batch of B rows (0 two-launch,
-// 1 single-pass, 3 the three-launch mode of the cascade alone).
+// 1 single-pass, 3 the three-launch mode).
 int chain_mode(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M, int64_t c, int S);
 size_t chain_tile_workspace_bytes(int64_t B, int64_t n_in, int64_t n_out, int K, int L, int M,
                                   int64_t c, int S);

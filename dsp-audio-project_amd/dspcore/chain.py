@@ -91,7 +91,7 @@ class Chain:
         S = self.eq.sos.shape[0]
         lib = _lib.load()
         self.tile_len = 0 if (self.identity_src and self.eq.bypass) else int(lib.dsp_chain_tile_len(
-            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S))
+            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S, self.B))
         # Two-launch path (other geometries, or dsp_chain_path(1)): x-domain chunk states (include/dspcore.h, dsp_chain_f32) need a chunk
         # length with chunk_len*M/L a multiple of 4; take it unless it would cut
         # the row into far fewer chunks than the plain rule.
@@ -100,7 +100,7 @@ class Chain:
         # (ops.forced_chain_path; the modes agree to float64 rounding only)
         self._force = ops.forced_chain_path(
             None if plan_batch is None or int(plan_batch) == self.B else int(plan_batch),
-            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S)
+            cfg.n_in, n_out, self.src.K, self.src.L, self.src.M, self.src.c_offset, S, self.B)
         plain = chunk_len_for(n_out, mc)
         eligible = (use_xstate and use_table and not self.identity_src and not self.eq.bypass
                     and 1 <= S <= 8 and S != 7)

@@ -218,18 +218,24 @@ def _eq_tile_plan(n: int, sos: np.ndarray, device: torch.device):
 
 
 class forced_chain_path:
-    """Sets dsp_chain_path on the calling thread to the path the default would
-    take for a batch of plan_batch rows (dsp_chain_mode: 2 chained tiles, 4 the
-    three-launch mode), unless a path is already forced; restores it after.
+    """Sets dsp_chain_path on the calling thread to the single-pass mode the
+    default takes for a batch of plan_batch rows (dsp_chain_mode: 2 chained
+    tiles, 4 the three-launch mode) where the call's own batch of B rows would
+    take the other one, unless a path is already forced; restores it after.
     Shards of one job use it so that every shard's rows are bitwise the
-    unsharded call's (the two modes agree to float64 rounding only)."""
+    unsharded call's (the two modes agree to float64 rounding only; chained
+    and persistent tiles are bitwise one, so a batch both would run chained
+    or persistent is left to the default)."""
 
     def __init__(self, plan_batch: int | None, n_in: int, n_out: int, K: int, L: int, M: int,
-                 c: int, S: int):
+                 c: int, S: int, B: int | None = None):
         self.path = None
         if plan_batch is not None:
-            mode = _lib.load().dsp_chain_mode(int(plan_batch), n_in, n_out, K, L, M, c, S)
-            self.path = 4 if mode == 3 else 2 if mode == 1 else None
+            lib = _lib.load()
+            mode = lib.dsp_chain_mode(int(plan_batch), n_in, n_out, K, L, M, c, S)
+            own = None if B is None else lib.dsp_chain_mode(int(B), n_in, n_out, K, L, M, c, S)
+            if mode != own:
+                self.path = 4 if mode == 3 else 2 if mode == 1 else None
 
     def __enter__(self):
         self.prev = None
@@ -273,7 +279,7 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     # zero-filled: the chained tiles' hand-off flags start clear (a completed
     # call leaves them clear; the cached allocator's block is not assumed so)
     ws = torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device)
-    force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S)
+    force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S, B)
     with torch.cuda.device(x.device), force:
         rc = lib.dsp_chain_f32(
             _ptr(x), None, _ptr(out), None, B, n, ld(x), n, ld(out), _ptr(taps), 1, 1, 1, 0,

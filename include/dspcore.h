@@ -311,12 +311,11 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * hand-off above), 3 the single-pass path with its persistent kernel where
  * one is built (L/M = 160/147: each wave runs its channels' tiles in order,
  * the entry state in registers; the default picks it for batches that fill
- * the chip), 4 (ABI 2.7) the three-launch mode of the cascade alone (the
- * one-tap SRC bypass above): every tile from a zero entry state, a scan of the
- * tiles' end states per channel, every tile again from its entry state -- no
- * tile waits for another; the default picks it for small batches of long
- * rows, where the chained hand-off (~2 us a tile) would bound the launch
- * (DESIGN.md §3.0.9); -1 only queries; returns the previous setting
+ * the chip), 4 (ABI 2.7) the three-launch mode of every single-pass kernel:
+ * every tile from a zero entry state, a scan of the tiles' end states per
+ * channel, every tile again from its entry state -- no tile waits for
+ * another; the default picks it for small batches of long rows, where the
+ * chained hand-off (~2 us a tile) would bound the launch; -1 only queries; returns the previous setting
  * (DSP_EINVAL for anything else).  Every variant gives bitwise the same y;
  * z agrees across variants to float64 rounding (bitwise for 2 and 3).
  * ------------------------------------------------------------------------- */
@@ -325,8 +324,7 @@ int64_t dsp_chain_tile_len(int64_t n_in, int64_t n_out, int32_t K, int32_t L, in
                            int64_t c_offset, int32_t S);
 /* (ABI 2.7, HOST) The path dsp_chain_f32 with dsp_chain_path 0 takes for a
  * batch of B rows of this geometry: 0 the two-launch chain, 1 a single-pass
- * kernel (chained tiles or persistent), 3 the three-launch mode of the cascade
- * alone.  A caller that shards one job's rows over several calls passes the
+ * kernel (chained tiles or persistent), 3 its three-launch mode.  A caller that shards one job's rows over several calls passes the
  * job's B and forces the answer (dsp_chain_path 2 for 1, 4 for 3) on every
  * shard, so that every shard's rows are bitwise the unsharded call's. */
 int32_t dsp_chain_mode(int64_t B, int64_t n_in, int64_t n_out, int32_t K, int32_t L, int32_t M,

@@ -374,3 +374,34 @@ def test_drop_in_host_conversions_match_numpy(gpu):
     for _ in range(3):                   # later calls do not touch a returned array
         dc._from_rows(torch.zeros_like(t), how, np.float64)
     np.testing.assert_array_equal(back, keep)
+
+
+@pytest.mark.parametrize("fs,L,M,K,B,n_in", [(44100, 160, 147, 1023, 1, 441000),
+                                             (48000, 5, 4, 31, 2, 96000)])
+def test_three_launch_mode_generic_kernels(gpu, fs, L, M, K, B, n_in):
+    """The three-launch mode on the generic single-pass kernels (160/147:
+    k_chain_gct3; others: k_chain_gen3): against the chained tiles (path 2) y
+    bitwise, z within 2e-6; the default takes it for a long channel or two;
+    rows against the oracle."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    cfg = ChainConfig(n_in, fs, L, M, K, orc.CONFIG3_GAINS, n_fft=4096)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 32
+    gen = torch.Generator(device=gpu).manual_seed(L + M + B)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0] *= 4.0
+    (y0, z0, m0), names0 = _traced(lambda: ch.run(x))
+    with _chain_path(2):
+        (y2, z2, m2), names2 = _traced(lambda: ch.run(x))
+    assert "chain_tile_agg" in names0 and "chain_tile_carry" in names0, names0
+    assert "chain_tile_agg" not in names2, names2
+    assert ch.handoff_ok()
+    assert torch.equal(y0, y2)
+    assert (z0 - z2).abs().max().item() <= 2e-6
+    assert (m0 - m2).abs().max().item() <= MAG_RTOL * m2.abs().max().item()
+    for b in range(B):
+        ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), fs, L, M, orc.CONFIG3_GAINS, K, 4096)
+        assert np.max(np.abs(y0[b].cpu().numpy() - ry)) <= 2e-6 * max(1.0, np.abs(ry).max())
+        assert np.max(np.abs(z0[b].cpu().numpy() - rz)) <= EQ_ATOL
+        assert np.max(np.abs(m0[b].cpu().numpy() - rmag)) <= MAG_RTOL * np.max(rmag)

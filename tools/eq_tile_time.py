@@ -47,16 +47,19 @@ def graph_ms(fn, reps):
 def main():
     args = sys.argv[1:]
     L = M = 1
-    if "--ratio" in args:   # another SRC ratio through the same three paths
+    K = None
+    if "--ratio" in args:   # another SRC ratio (L/M or L/M/K) through the same paths
         i = args.index("--ratio")
-        L, M = (int(v) for v in args[i + 1].split("/"))
+        v = [int(t) for t in args[i + 1].split("/")]
+        L, M = v[0], v[1]
+        K = v[2] if len(v) > 2 else None
         del args[i:i + 2]
     shapes = [tuple(int(v) for v in a.split("x")) for a in args] or \
         [(4096, 48000), (32768, 48000), (1, 441000), (1, 48000), (16, 441000)]
     dev = torch.device("cuda", 0)
-    print(f"L/M {L}/{M}", flush=True)
+    print(f"L/M {L}/{M}" + (f" K {K}" if K else ""), flush=True)
     for B, n in shapes:
-        cfg = ChainConfig(n, 48000, L, M, None, GAINS, n_fft=4096)
+        cfg = ChainConfig(n, 48000, L, M, K, GAINS, n_fft=4096)
         ch = Chain(cfg, B, dev, keep_y=False)
         x = torch.rand((B, n), device=dev) * 2 - 1
         reps = max(5, min(200, int(2e9 // (B * n * 8))))

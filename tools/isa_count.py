@@ -8,7 +8,7 @@ maintenance): a quick check of what a source change did to a kernel.
 
 --check-handoff (run by __graft_entry__.build()): the single-pass chain kernels
 (k_chain_tile, k_chain_gct, k_chain_gen, k_chain_pp; not their rare-path repair kernels,
-whose timing does not matter, nor the three-launch mode's k_chain_pp3 / k_chain_tile3, which have no
+whose timing does not matter, nor the three-launch mode's k_chain_*3 kernels, which have no
 hand-off) must issue their SRC and pass-1 work
 before the tile hand-off wait (csrc/chain_tile.hip, tile_cascade): no
 v_pk_fma_f32 (the SRC's and pass 1's packed FMAs) after the poll loop's first
@@ -131,10 +131,10 @@ def check_handoff(path, text=None):
     heads = [(m.start(), m.group(1)) for m in re.finditer(r"^(_Z\w+):", s, re.M)]
     bad, seen, report = [], 0, []
     for i, (pos, name) in enumerate(heads):
-        # (k_chain_pp3 / k_chain_tile3: launches 1 and 3 of the three-launch
+        # (k_chain_{pp,tile,gen,gct}3: launches 1 and 3 of the three-launch
         # mode, which wait for no other tile)
         if not re.search(r"k_chain_(tile|gct|gen|pp)", name) or "_repair" in name or \
-                re.search(r"k_chain_(pp|tile)3", name):
+                re.search(r"k_chain_(pp|tile|gen|gct)3", name):
             continue
         seen += 1
         end = heads[i + 1][0] if i + 1 < len(heads) else len(s)
