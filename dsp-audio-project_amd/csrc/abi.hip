@@ -85,7 +85,7 @@ int dsp_version(void) {
   // single-pass chain kernels for every app ratio (round 6).
   // 2.7.0: dsp_chain_f32 takes the SRC bypass as the one-tap SRC (L = M = 1,
   // K = 1) single-pass, and mag == NULL skips the spectrum; dsp_chain_path 4;
-  // dsp_chain_mode (round 6).
+  // dsp_chain_mode; dsp_convert_f64_f32 / dsp_convert_f32_f64 (round 6).
   return 20700;
 }
 
@@ -332,6 +332,16 @@ int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64
   dsp::clear_error();
   return dsp::launch_quantize_pcm16(z, out, B, n, ld_z, ld_out, peak_out, precision,
                                     static_cast<hipStream_t>(stream));
+}
+
+int dsp_convert_f64_f32(const double* in, float* out, int64_t n, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_convert_f64_f32(in, out, n, static_cast<hipStream_t>(stream));
+}
+
+int dsp_convert_f32_f64(const float* in, double* out, int64_t n, void* stream) {
+  dsp::clear_error();
+  return dsp::launch_convert_f32_f64(in, out, n, static_cast<hipStream_t>(stream));
 }
 
 int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,

@@ -658,6 +658,38 @@ int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double thr
   });
 }
 
+// Host <-> device dtype edges of the drop-in (modules/dsp_core.py): numpy's
+// float64 arrays narrowed to the kernels' float32 and their float32 results
+// widened back, on the device (round to nearest even, as numpy's astype;
+// float32 -> float64 is exact).  Flat arrays, 16-byte vectors where both
+// pointers allow, grid-stride.
+template <class TI, class TO>
+__global__ __launch_bounds__(kIoNT) void k_convert(const TI* __restrict__ in, TO* __restrict__ out,
+                                                   int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kIoNT;
+  for (int64_t i = (int64_t)blockIdx.x * kIoNT + threadIdx.x; i < n; i += stride)
+    out[i] = (TO)in[i];
+}
+
+template <class TI, class TO>
+int launch_convert(const TI* in, TO* out, int64_t n, hipStream_t s) {
+  DSP_REQUIRE(n >= 0, "bad size");
+  if (n == 0) return DSP_OK;
+  DSP_REQUIRE(in && out, "null pointer");
+  const int64_t blocks = std::min<int64_t>(ceil_div(n, (int64_t)kIoNT), 8192);
+  TraceScope trace("convert", s);
+  hipLaunchKernelGGL((k_convert<TI, TO>), dim3((unsigned)blocks), dim3(kIoNT), 0, s, in, out, n);
+  DSP_LAUNCHED("k_convert");
+  return DSP_OK;
+}
+
+int launch_convert_f64_f32(const double* in, float* out, int64_t n, hipStream_t s) {
+  return launch_convert(in, out, n, s);
+}
+int launch_convert_f32_f64(const float* in, double* out, int64_t n, hipStream_t s) {
+  return launch_convert(in, out, n, s);
+}
+
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
                           int64_t ld_out, uint32_t* peak, int precision, hipStream_t s) {
   DSP_REQUIRE(B >= 0 && n >= 0 && ld_z >= n && ld_out >= n, "bad sizes");

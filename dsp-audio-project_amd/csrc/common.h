@@ -283,6 +283,8 @@ int launch_pcm_batch(const void* pcm, size_t pcm_bytes, const dsp_pcm_row* rows,
                      uint32_t* peak_out, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_peak_normalize(float* x, int64_t B, int64_t n, int64_t ld, double threshold,
                           uint32_t* peak, hipStream_t s);
+int launch_convert_f64_f32(const double* in, float* out, int64_t n, hipStream_t s);
+int launch_convert_f32_f64(const float* in, double* out, int64_t n, hipStream_t s);
 int launch_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
                           int64_t ld_out, uint32_t* peak, int precision, hipStream_t s);
 

@@ -74,6 +74,8 @@ _SIGNATURES = {
     "dsp_chain_path": (ctypes.c_int, [_c_i32]),
     "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_chain_mode": (_c_i32, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
+    "dsp_convert_f64_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
+    "dsp_convert_f32_f64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,
                                           _c_i64, _c_i32, _c_i64]),
     "dsp_chain_xstate_geometry": (ctypes.c_int, [

@@ -121,6 +121,35 @@ def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = No
     return out
 
 
+_NARROW = {torch.float64: torch.float32, torch.complex128: torch.complex64}
+_WIDEN = {torch.float32: torch.float64, torch.complex64: torch.complex128}
+
+
+def convert(x: torch.Tensor, dtype: torch.dtype, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x cast to `dtype` on the device by the library (dsp_convert_f64_f32 /
+    dsp_convert_f32_f64: numpy's astype rounding), for the float64 <-> float32
+    and complex128 <-> complex64 pairs; a contiguous copy of x keeps its
+    shape."""
+    if x.dtype == dtype:
+        return x
+    if _NARROW.get(x.dtype) == dtype:
+        fn = "dsp_convert_f64_f32"
+    elif _WIDEN.get(x.dtype) == dtype:
+        fn = "dsp_convert_f32_f64"
+    else:
+        raise ValueError(f"no library conversion {x.dtype} -> {dtype}")
+    if not x.is_cuda:
+        raise ValueError("x must be a CUDA (ROCm) tensor")
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    n = x.numel() * (2 if x.is_complex() else 1)
+    with torch.cuda.device(x.device):
+        rc = getattr(_lib.load(), fn)(_ptr(x), _ptr(out), n, _stream(x.device))
+    _lib.check(rc, fn)
+    return out
+
+
 def biquad_workspace(B: int, n: int, S: int, device: torch.device,
                      chunk_len: int | None = None) -> torch.Tensor:
     chunk_len = chunk_len_for(n, max_chunks_for(B)) if chunk_len is None else chunk_len
@@ -248,15 +277,42 @@ class forced_chain_path:
             _lib.chain_path(self.prev)
 
 
+_eq_ws_lock = threading.Lock()
+_eq_ws: OrderedDict = OrderedDict()   # (device, stream, thread, bytes) -> zero-filled workspace
+EQ_WS_CACHE_MAX = 16
+
+
+def _eq_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """A chain workspace of at least nbytes for the calling thread's current
+    stream, zero-filled once and reused: every call that completes leaves its
+    hand-off flags clear (include/dspcore.h), and calls of one thread on one
+    stream run in order."""
+    key = (device.index, _stream(device), threading.get_ident(), int(nbytes))
+    with _eq_ws_lock:
+        ws = _eq_ws.get(key)
+        if ws is not None:
+            _eq_ws.move_to_end(key)
+            return ws
+    ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+    with _eq_ws_lock:
+        ws = _eq_ws.setdefault(key, ws)
+        _eq_ws.move_to_end(key)
+        while len(_eq_ws) > EQ_WS_CACHE_MAX:
+            _eq_ws.popitem(last=False)
+    return ws
+
+
 def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = None,
-                   plan_batch: int | None = None) -> torch.Tensor | None:
+                   plan_batch: int | None = None, check: bool = False) -> torch.Tensor | None:
     """z = clip(cascade(x)) per row (dsp_core.py:233-254) through the
     single-pass kernel of the cascade alone: dsp_chain_f32 with the SRC bypass
     as the one-tap SRC (L = M = 1, K = 1, tap 1.0), y = NULL, mag = NULL -- x
     read once, z written once; small batches of long rows take its
     three-launch mode (the library picks it, for plan_batch rows when given:
     forced_chain_path).  Returns None where that kernel does not serve the
-    call (biquad_cascade does)."""
+    call (biquad_cascade does) -- and, with check (it synchronises the
+    stream), where a chained tile's hand-off wait gave up (dsp_chain_status;
+    the workspace is reset): the caller reruns the rows on biquad_cascade."""
     x = _rows(x, "x")
     if x.dtype != torch.float32:
         x = x.float()
@@ -276,16 +332,21 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     S = sos.shape[0]
     chunk = chunk_len_for(n, max_chunks_for(B))
     ws_bytes = int(lib.dsp_chain_workspace_bytes(B, n, n, 1, 1, 1, 0, S, chunk))
-    # zero-filled: the chained tiles' hand-off flags start clear (a completed
-    # call leaves them clear; the cached allocator's block is not assumed so)
-    ws = torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device)
+    ws = _eq_workspace(x.device, ws_bytes)
     force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S, B)
     with torch.cuda.device(x.device), force:
         rc = lib.dsp_chain_f32(
             _ptr(x), None, _ptr(out), None, B, n, ld(x), n, ld(out), _ptr(taps), 1, 1, 1, 0,
             _lib.sos_pointer(sos), S, 1, chunk, None, None, 0, _ptr(tables), key, 0, 0, 0, 0,
             None, None, _ptr(ws), ws.numel(), _stream(x.device))
-    _lib.check(rc, "dsp_chain_f32")
+        _lib.check(rc, "dsp_chain_f32")
+        if check:
+            st = lib.dsp_chain_status(_ptr(ws), ws.numel(), 0, _stream(x.device))
+            if st < 0:
+                _lib.check(st, "dsp_chain_status")
+            if st:
+                lib.dsp_chain_status(_ptr(ws), ws.numel(), 1, _stream(x.device))
+                return None
     return out
 
 

@@ -85,12 +85,13 @@ def _to_rows(x, complex_ok=False):
     how = "np1" if a.ndim == 1 else "np2"
     a2 = a.reshape(1, -1) if a.ndim == 1 else a
     cplx = complex_ok and np.iscomplexobj(a2)
-    del ops
     if a2.flags.c_contiguous and a2.dtype == (np.complex128 if cplx else np.float64):
         # float64 / complex128 rows (what the reference's functions return and
-        # app.py passes on): copied as stored and narrowed on the device --
-        # numpy's astype rounding, without a fresh host array to fault in
-        return torch.from_numpy(a2).to(dev).to(torch.complex64 if cplx else torch.float32), how
+        # app.py passes on): copied as stored and narrowed on the device by the
+        # library (ops.convert: numpy's astype rounding), without a fresh host
+        # array to fault in
+        return ops.convert(torch.from_numpy(a2).to(dev),
+                           torch.complex64 if cplx else torch.float32), how
     host = np.ascontiguousarray(a2, dtype=np.complex64 if cplx else np.float32)
     return torch.from_numpy(host).to(dev), how
 
@@ -111,9 +112,9 @@ def _from_rows(t, how, np_dtype):
     if tdt is None or t.numel() * tdt.itemsize > PINNED_MAX_BYTES:
         host = t.cpu().numpy().astype(np_dtype)
     else:
-        # widened on the device (float32 -> float64 is exact), one copy into a
-        # pinned buffer that the returned array keeps alive
-        src = t if t.dtype == tdt else t.to(tdt)
+        # widened on the device by the library (float32 -> float64 is exact),
+        # one copy into a pinned buffer that the returned array keeps alive
+        src = t if t.dtype == tdt else _ops().convert(t, tdt)
         pinned = torch.empty(tuple(src.shape), dtype=tdt, pin_memory=True)
         pinned.copy_(src)
         host = pinned.numpy()
@@ -359,6 +360,9 @@ def sistema_ecualizador(x_n, fs, ganancias_bandas):
         # the single-pass cascade alone where it serves the rows (x read once,
         # z written once; one long channel takes its three-launch mode), else
         # the two-pass cascade
-        z = ops.eq_single_pass(t, plan.sos, plan_batch=B) if plan.sos.shape[0] else None
+        # (numpy in: the hand-off status is read, as the result is synchronised
+        # anyway; a tensor call stays asynchronous)
+        z = (ops.eq_single_pass(t, plan.sos, plan_batch=B, check=not _is_tensor(x_n))
+             if plan.sos.shape[0] else None)
         return z if z is not None else _cascade(ops, t, plan.sos, True, B)
     return _run(x_n, run, out_dtype)

@@ -437,6 +437,11 @@ int dsp_pcm_batch_to_mono_f32(const void* pcm, size_t pcm_bytes, const dsp_pcm_r
                               int64_t B, int64_t width, float* out, int64_t ld_out,
                               double threshold, uint32_t* peak_out, void* workspace,
                               size_t workspace_bytes, void* stream);
+/* (ABI 2.7) DEVICE dtype edges of the drop-in: out[i] = in[i] for i < n over
+ * flat arrays, float64 -> float32 rounded to nearest even (numpy's astype) or
+ * float32 -> float64 (exact); complex arrays pass as 2n reals. */
+int dsp_convert_f64_f32(const double* in, float* out, int64_t n, void* stream);
+int dsp_convert_f32_f64(const float* in, double* out, int64_t n, void* stream);
 int dsp_quantize_pcm16(const float* z, int16_t* out, int64_t B, int64_t n, int64_t ld_z,
                        int64_t ld_out, uint32_t* peak_out, int32_t precision, void* stream);
 int dsp_wav_header_pcm16(uint8_t* header44, int32_t sample_rate, int32_t channels,

@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 32
+    assert len(names) == 34
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"

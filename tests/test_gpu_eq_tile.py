@@ -405,3 +405,57 @@ def test_three_launch_mode_generic_kernels(gpu, fs, L, M, K, B, n_in):
         assert np.max(np.abs(y0[b].cpu().numpy() - ry)) <= 2e-6 * max(1.0, np.abs(ry).max())
         assert np.max(np.abs(z0[b].cpu().numpy() - rz)) <= EQ_ATOL
         assert np.max(np.abs(m0[b].cpu().numpy() - rmag)) <= MAG_RTOL * np.max(rmag)
+
+
+def test_drop_in_equaliser_handoff_give_up_falls_back(gpu):
+    """The drop-in's single-pass cascade reads the hand-off status for numpy
+    calls: with every wait giving up at once (spin limit 0, chained tiles
+    forced) it resets the workspace and reruns the rows on the two-pass
+    cascade, so the result is still the reference's; the next call is clean."""
+    from dspcore import _lib
+    from oracle import dsp_ref_cpu as orc
+    import modules.dsp_core as dc
+    x = np.random.default_rng(9).uniform(-1, 1, (4, 48000)) * 0.8
+    ref = np.stack([orc.equaliser(r, 48000, orc.CONFIG3_GAINS) for r in x])
+    prev = _lib.spin_limit(0)
+    try:
+        with _chain_path(2):
+            z = dc.sistema_ecualizador(x, 48000, orc.CONFIG3_GAINS)
+    finally:
+        _lib.spin_limit(prev)
+    assert np.max(np.abs(z - ref)) <= EQ_ATOL
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    try:
+        with _chain_path(2):
+            z2 = dc.sistema_ecualizador(x, 48000, orc.CONFIG3_GAINS)
+        names = [nm for nm, _ in _lib.trace_read()]
+    finally:
+        _lib.trace_enable(False)
+    assert "chain_tile" in names and not any(nm.startswith("iir") for nm in names), names
+    assert np.max(np.abs(z2 - ref)) <= EQ_ATOL
+
+
+def test_library_dtype_conversions(gpu):
+    """ops.convert (dsp_convert_f64_f32 / dsp_convert_f32_f64): numpy's astype
+    bits both ways, real and complex, odd lengths; no torch kernel."""
+    from dspcore import _lib, ops
+    rng = np.random.default_rng(2)
+    a = rng.standard_normal(10007) * np.logspace(-45, 38, 10007)
+    t = torch.from_numpy(a).to(gpu)
+    _lib.trace_enable(True)
+    _lib.trace_read()
+    try:
+        f = ops.convert(t, torch.float32)
+        d = ops.convert(f, torch.float64)
+        names = [nm for nm, _ in _lib.trace_read()]
+    finally:
+        _lib.trace_enable(False)
+    assert names == ["convert", "convert"], names
+    np.testing.assert_array_equal(f.cpu().numpy().view(np.uint32), a.astype(np.float32).view(np.uint32))
+    np.testing.assert_array_equal(d.cpu().numpy(), a.astype(np.float32).astype(np.float64))
+    c = (a[:5000] + 1j * a[5000:10000]).reshape(50, 100)
+    tc = ops.convert(torch.from_numpy(c).to(gpu), torch.complex64)
+    assert tc.shape == (50, 100)
+    np.testing.assert_array_equal(tc.cpu().numpy().view(np.uint32),
+                                  c.astype(np.complex64).view(np.uint32))
