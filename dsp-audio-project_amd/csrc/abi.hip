@@ -85,7 +85,9 @@ int dsp_version(void) {
   // single-pass chain kernels for every app ratio (round 6).
   // 2.7.0: dsp_chain_f32 takes the SRC bypass as the one-tap SRC (L = M = 1,
   // K = 1) single-pass, and mag == NULL skips the spectrum; dsp_chain_path 4;
-  // dsp_chain_mode; dsp_convert_f64_f32 / dsp_convert_f32_f64 (round 6).
+  // dsp_chain_mode; dsp_convert_f64_f32 / dsp_convert_f32_f64; FFTs of 2^31
+  // and 2^32 points (DSP_MAX_LOG2N_FFT 32, DSP_MAX_LOG2N_FOURSTEP 30) and the
+  // dsp_fft_split_log2n test hook (round 6).
   return 20700;
 }
 
@@ -127,6 +129,14 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
 
 size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n) {
   return dsp::fft_workspace_bytes(B, log2n);
+}
+
+int dsp_fft_split_log2n(int32_t log2n) {
+  dsp::clear_error();
+  if (log2n < -1 || (log2n >= 0 && (log2n < DSP_MAX_LOG2N + 2 || log2n > DSP_MAX_LOG2N_FOURSTEP + 1)))
+    return dsp::set_error(DSP_EINVAL, "split log2n %d not in [%d, %d]", log2n, DSP_MAX_LOG2N + 2,
+                          DSP_MAX_LOG2N_FOURSTEP + 1);
+  return dsp::fft_split_log2n(log2n);
 }
 
 int dsp_fft_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,

@@ -244,6 +244,16 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
                int64_t ld_in, int64_t ld_out, const float* tw, void* ws, size_t ws_bytes,
                hipStream_t s);
 size_t fft_workspace_bytes(int64_t B, int log2n);
+size_t fourstep_workspace_bytes(int64_t B, int log2n);
+// Above one four-step transform (fft_split.hip): the reference's top radix-2
+// level (even / odd halves, then the butterfly); fft_split_log2n sets the
+// calling thread's smallest log2n that takes it (a test hook; default
+// DSP_MAX_LOG2N_FOURSTEP + 1) and returns the previous one.
+bool fft_takes_split(int log2n);
+int fft_split_log2n(int log2n);
+size_t fft_split_workspace_bytes(int log2n);
+int launch_fft_split(const float* in, float* out, int64_t B, int log2n, int real_in, int64_t ld_in,
+                     int64_t ld_out, const float* tw, void* ws, size_t ws_bytes, hipStream_t s);
 
 // Non-finite input through the power-of-two FFT / spectrum (fft_nf.hip): the
 // reference's inf / NaN labels restored after the fast transform.  mode: 0

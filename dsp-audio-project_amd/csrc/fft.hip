@@ -938,7 +938,7 @@ int launch_spec_wave12(const FftArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// Four-step FFT for N = 2^15 .. 2^DSP_MAX_LOG2N_FFT (beyond one workgroup's
+// Four-step FFT for N = 2^15 .. 2^DSP_MAX_LOG2N_FOURSTEP (beyond one workgroup's
 // LDS): N = NA * NB, n = n1 + NB n2, k = k2 + NA k1 (n1, k1 < NB; n2, k2 < NA)
 //   step A: Y[n1][k2] = W_N^(n1 k2) * sum_n2 x[n1 + NB n2] W_NA^(n2 k2)
 //           -> workspace[k2][n1]
@@ -1221,7 +1221,7 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
     case 20: return launch_fft4<10, 10, MODE>(f, s);
     case 21: return launch_fft4<10, 11, MODE>(f, s);
     case 22: return launch_fft4<11, 11, MODE>(f, s);  // (2^23 and up: run_fft6_row)
-    default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
+    default: return set_error(DSP_EINVAL, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FOURSTEP);
   }
 }
 
@@ -1244,7 +1244,7 @@ int dispatch4(const Fft4Args& f, int log2n, hipStream_t s) {
 // 0.092 vs 0.111 ms at 2^23, 0.211 vs 0.274 at 2^24 and the two-pass faster at
 // 2^22, 0.052 vs 0.057 ms (profiles/r05_fft_large.txt).
 constexpr int kLog2Nested = 23;
-static_assert(kLog2Nested > DSP_MAX_LOG2N + 1 && kLog2Nested <= DSP_MAX_LOG2N_FFT, "nest from");
+static_assert(kLog2Nested > DSP_MAX_LOG2N + 1 && kLog2Nested <= DSP_MAX_LOG2N_FOURSTEP, "nest from");
 
 template <int LA, int LA1, int LB2, int MODE>
 int run_fft6_row(const FftArgs& row, float2* Y, float2* Y2, const float2* twc, uint32_t* hdr,
@@ -1467,12 +1467,23 @@ constexpr int64_t kMaxRows4 = 65535;  // grid y extent of the four-step kernels
 // time): [Y: N][Y': N complex][coarse twiddles][header: 2 words per row].
 // The coarse twiddle table (tw_fetch) above 2^20 points: 2^floor(log2n / 2)
 // complex.
-size_t fft_workspace_bytes(int64_t B, int log2n) {
-  if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
+size_t fourstep_workspace_bytes(int64_t B, int log2n) {
+  if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FOURSTEP) return 0;
   const bool three = log2n >= kLog2Nested;
   const size_t rows = three ? (size_t)B : (size_t)(B < kMaxRows4 ? B : kMaxRows4);
   const size_t data = mul_sat(three ? 2 : (size_t)B, (size_t)1 << log2n, sizeof(float2));
   return add_sat(add_sat(data, tw_coarse_bytes(log2n)), mul_sat(rows, 2, sizeof(uint32_t)));
+}
+
+// The FFT's workspace (dsp_fft_workspace_bytes): the four-step's for one
+// transform, the radix-2 split's (fft_split.hip) above it -- the larger of the
+// two where a test hook (dsp_fft_split_log2n) sends four-step sizes through
+// the split.
+size_t fft_workspace_bytes(int64_t B, int log2n) {
+  if (B <= 0 || log2n <= DSP_MAX_LOG2N || log2n > DSP_MAX_LOG2N_FFT) return 0;
+  const size_t four = fourstep_workspace_bytes(B, log2n);
+  const size_t split = fft_takes_split(log2n) ? fft_split_workspace_bytes(log2n) : 0;
+  return four > split ? four : split;
 }
 
 namespace {
@@ -1480,8 +1491,9 @@ namespace {
 // Four-step transform of B rows, in launches of <= kMaxRows4 rows.
 template <int MODE>
 int run_fft4(FftArgs a, int log2n, void* ws, size_t ws_bytes, hipStream_t s) {
-  DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n, DSP_MAX_LOG2N_FFT);
-  const size_t need = fft_workspace_bytes(a.B, log2n);
+  DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FOURSTEP, "log2n=%d outside [0, %d]", log2n,
+              DSP_MAX_LOG2N_FOURSTEP);
+  const size_t need = fourstep_workspace_bytes(a.B, log2n);
   DSP_REQUIRE(ws && ws_bytes >= need, "FFT workspace too small: %zu < %zu bytes", ws_bytes, need);
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 7) == 0, "FFT workspace not 8-byte aligned");
   const int64_t B = a.B;
@@ -1536,8 +1548,8 @@ int launch_spectrum(const float* x, float* mag, int64_t B, int64_t ld_x,
                     int64_t ld_mag, const float* window, const float* tw,
                     void* ws, size_t ws_bytes, hipStream_t s, bool repair) {
   if (log2n > DSP_MAX_LOG2N) {
-    DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FFT, "log2n=%d outside [0, %d]", log2n,
-                DSP_MAX_LOG2N_FFT);
+    DSP_REQUIRE(log2n <= DSP_MAX_LOG2N_FOURSTEP, "log2n=%d outside [0, %d]", log2n,
+                DSP_MAX_LOG2N_FOURSTEP);
     const int64_t N = int64_t(1) << log2n;
     DSP_REQUIRE(B >= 0 && seg_start >= 0 && seg_len >= 0 && seg_len <= N,
                 "bad segment start=%lld len=%lld (N=%lld)", (long long)seg_start,
@@ -1596,6 +1608,8 @@ int launch_fft(const float* in, float* out, int64_t B, int log2n, int real_in,
   DSP_REQUIRE((reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
                   (real_in || (reinterpret_cast<uintptr_t>(in) & 7) == 0),
               "complex buffers must be 8-byte aligned");
+  if (fft_takes_split(log2n))  // above one four-step transform (fft_split.hip)
+    return launch_fft_split(in, out, B, log2n, real_in, ld_in, ld_out, tw, ws, ws_bytes, s);
   FftArgs a{in, out, B, ld_in, ld_out, 0, 0, 0, 1, nullptr, reinterpret_cast<const float2*>(tw)};
   if (log2n > DSP_MAX_LOG2N) {
     TraceScope trace("fft", s);

@@ -257,7 +257,7 @@ int launch_nf_small(const NfArgs& a, hipStream_t s) {
 
 int launch_nf_large(const NfArgs& a, uint32_t* hdr, uint64_t* lists, int64_t list_stride,
                     hipStream_t s) {
-  DSP_REQUIRE(a.log2n > DSP_MAX_LOG2N && a.log2n <= DSP_MAX_LOG2N_FFT,
+  DSP_REQUIRE(a.log2n > DSP_MAX_LOG2N && a.log2n <= DSP_MAX_LOG2N_FOURSTEP,
               "non-finite repair: log2n=%d", a.log2n);
   if (a.B == 0) return DSP_OK;
   DSP_REQUIRE(a.B <= 65535, "non-finite repair: %lld rows per launch", (long long)a.B);

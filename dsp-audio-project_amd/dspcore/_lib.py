@@ -29,7 +29,8 @@ DSP_EHIP = -2
 DSP_ENOTSUP = -3
 DSP_MAX_STAGES = 16
 DSP_MAX_LOG2N = 14
-DSP_MAX_LOG2N_FFT = 30
+DSP_MAX_LOG2N_FOURSTEP = 30
+DSP_MAX_LOG2N_FFT = 32
 DSP_MAX_DFT = 8192
 DSP_LFILTER_NF_MAX = 4096
 
@@ -75,6 +76,7 @@ _SIGNATURES = {
     "dsp_chain_tile_len": (_c_i64, [_c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_chain_mode": (_c_i32, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _c_i32]),
     "dsp_convert_f64_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
+    "dsp_fft_split_log2n": (ctypes.c_int, [_c_i32]),
     "dsp_convert_f32_f64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
     "dsp_chain_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32,
                                           _c_i64, _c_i32, _c_i64]),

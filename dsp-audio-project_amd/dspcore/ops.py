@@ -453,7 +453,7 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
     if x.dtype != torch.float32:
         x = x.float()
     B = x.shape[0]
-    lg = _log2(n_fft)
+    lg = _log2(n_fft, _lib.DSP_MAX_LOG2N_FOURSTEP)
     if out is None:
         out = torch.empty((B, n_fft // 2 + 1), dtype=torch.float32, device=x.device)
     win = _table("hann", n_fft, x.device)

@@ -30,7 +30,7 @@ Deliberate differences, documented in DESIGN.md:
   the tolerances of tests/ (SRC atol 2e-6, EQ atol 1e-5, FFT 1e-5 * max|X|);
 * fft_diezmado_en_tiempo raises ValueError for every length that is not a
   power of two (the reference raises for most and returns a wrong-length
-  array for N = 3), and RuntimeError above 2^30 points (the reference's
+  array for N = 3), and RuntimeError above 2^32 points (the reference's
   pure-Python recursion has no limit but takes hours there);
 * keyword-only extensions: conversion_tasa_muestreo(..., num_taps=None) and
   calcular_espectro_magnitud(..., n_fft=2048); one added function,
@@ -222,11 +222,12 @@ def cargar_senal_audio(buffer_archivo):
 def fft_diezmado_en_tiempo(x):
     """Radix-2 decimation-in-time FFT (dsp_core.py:41-66), batched HIP kernel.
 
-    Length <= 1 returns x unchanged (:52).  Power-of-two lengths up to 2^30
+    Length <= 1 returns x unchanged (:52).  Power-of-two lengths up to 2^32
     give the natural-order DFT (complex128 for numpy input): one LDS-resident
     launch up to 2^14, a four-step transform (two launches, three from 2^23)
-    above.  Other lengths raise ValueError; powers of two above 2^30 raise
-    RuntimeError.
+    up to 2^30, and above it the reference's own top radix-2 level around two
+    transforms of half the length (csrc/fft_split.hip).  Other lengths raise
+    ValueError; powers of two above 2^32 raise RuntimeError.
     """
     n = _length(x)
     if n <= 1:

@@ -37,7 +37,10 @@ extern "C" {
 
 #define DSP_MAX_STAGES 16 /* biquad stages per cascade call                   */
 #define DSP_MAX_LOG2N 14  /* largest FFT handled in one LDS-resident launch   */
-#define DSP_MAX_LOG2N_FFT 30 /* largest FFT / spectrum (four-step above 2^14)  */
+#define DSP_MAX_LOG2N_FOURSTEP 30 /* largest spectrum, and largest FFT in one
+                                     four-step transform (above 2^14)            */
+#define DSP_MAX_LOG2N_FFT 32 /* largest FFT (ABI 2.7: the reference's radix-2
+                                split into two transforms above 2^30)            */
 #define DSP_MAX_DFT 8192  /* largest any-length DFT (Bluestein, M <= 2^14)     */
 #define DSP_LFILTER_NF_MAX 4096 /* largest order dsp_lfilter_nonfinite_f32 takes */
 
@@ -139,10 +142,20 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
  * (ABI 2.5, up to 2^30) three launches (a four-step nested in step B) row by
  * row, 2 * N * 8 bytes whatever B; plus, above 2^20, a coarse twiddle table of
  * 2^floor(log2n / 2) * 8 bytes, and a header of 8 bytes per row (per launch
- * part of at most 65535 rows for two launches).  Size the workspace with
+ * part of at most 65535 rows for two launches).  Above DSP_MAX_LOG2N_FOURSTEP
+ * (ABI 2.7, 2^31 and 2^32) the reference's own top level: each row's even and
+ * odd samples gathered into the workspace, transformed (as above; 2^32 splits
+ * once more), and combined in place, X[k] = E[k] + W^k O[k], X[k + N/2] =
+ * E[k] - W^k O[k] with W from the caller's table; the workspace (256-byte
+ * aligned) then holds the halves, an N/2-point twiddle table and the halves'
+ * own workspace, ~9 N complex-float bytes whatever B.  Size the workspace with
  * dsp_fft_workspace_bytes, never with a formula of your own: the size grew in
- * ABI 2.4 (per-row header) and 2.5 (coarse table, three-pass rows), and a
- * smaller buffer is refused with DSP_EINVAL.
+ * ABI 2.4 (per-row header), 2.5 (coarse table, three-pass rows) and 2.7 (the
+ * split), and a smaller buffer is refused with DSP_EINVAL.
+ * dsp_fft_split_log2n(log2n) (a test hook) sets the calling thread's smallest
+ * log2n (>= 16) that takes the split, default DSP_MAX_LOG2N_FOURSTEP + 1, so
+ * the split can be checked against one four-step transform; -1 queries;
+ * returns the previous value.
  * Non-finite input (ABI 2.4): every output component gets the class --
  * finite, +inf, -inf or NaN -- that the reference's recursive radix-2 DIT in
  * complex128 numpy arithmetic gives it (inf * 0 = NaN at the k = 0 twiddles,
@@ -155,6 +168,7 @@ int dsp_lfilter_nonfinite_f32(const float* x, float* y, int64_t B, int64_t n, in
  * (hypot) gives it (dsp_core.py:91).
  * ------------------------------------------------------------------------- */
 size_t dsp_fft_workspace_bytes(int64_t B, int32_t log2n);
+int dsp_fft_split_log2n(int32_t log2n);
 int dsp_fft_c2c_f32(const float* in, float* out, int64_t B, int32_t log2n,
                        int32_t real_input, int64_t ld_in, int64_t ld_out,
                        const float* twiddles, void* workspace, size_t workspace_bytes,
@@ -182,7 +196,7 @@ int dsp_dft_f32(const float* in, float* out, int64_t B, int64_t n, int32_t real_
  * Replaces dsp_core.py:74-98 (calcular_espectro_magnitud): segment
  * x[seg_start : seg_start + seg_len] zero-padded to N = 2^log2n (:76-82),
  * times window[N] (Hann, :85-87), FFT (:90), |X[k]| for k <= N/2 (:91,:97-98).
- * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.  log2n <= DSP_MAX_LOG2N_FFT;
+ * mag is float32 [B][ld_mag], ld_mag >= N/2 + 1.  log2n <= DSP_MAX_LOG2N_FOURSTEP;
  * above DSP_MAX_LOG2N the workspace rules of dsp_fft_c2c_f32 apply.
  * ------------------------------------------------------------------------- */
 int dsp_spectrum_f32(const float* x, float* mag, int64_t B, int64_t ld_x,

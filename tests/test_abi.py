@@ -10,7 +10,7 @@ from dspcore import _lib
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
     names = _lib.header_symbols()
-    assert len(names) == 34
+    assert len(names) == 35
     for name in names:
         assert hasattr(lib, name), name
         assert name in _lib._SIGNATURES, f"{name} has no ctypes signature"
@@ -42,7 +42,26 @@ def test_invalid_arguments_are_rejected_before_any_launch():
     assert lib.dsp_fft_workspace_bytes(1, 28) == 2 * (1 << 28) * 8 + (1 << 14) * 8 + 8
     assert lib.dsp_fft_workspace_bytes(1, 29) == 2 * (1 << 29) * 8 + (1 << 14) * 8 + 8
     assert lib.dsp_fft_workspace_bytes(5, 30) == 2 * (1 << 30) * 8 + (1 << 15) * 8 + 5 * 8
-    assert lib.dsp_fft_workspace_bytes(1, 31) == 0
+    # 2^31, 2^32 (ABI 2.7): the radix-2 split -- even / odd halves, an N/2-point
+    # twiddle table, the halves' own workspace (2^32 splits once more)
+    G = 1 << 30
+    w31 = 2 * (G * 8) + (G // 2) * 8 + lib.dsp_fft_workspace_bytes(1, 30) + 255
+    assert lib.dsp_fft_workspace_bytes(1, 31) == w31
+    assert lib.dsp_fft_workspace_bytes(7, 31) == w31                 # rows one at a time
+    assert lib.dsp_fft_workspace_bytes(1, 32) == 2 * (2 * G * 8) + G * 8 + w31 + 255
+    assert lib.dsp_fft_workspace_bytes(1, 33) == 0
+    # the test hook sends four-step sizes through the split (the larger
+    # workspace of the two), and answers the range
+    prev = lib.dsp_fft_split_log2n(-1)
+    assert prev == 31
+    assert lib.dsp_fft_split_log2n(15) == _lib.DSP_EINVAL
+    assert lib.dsp_fft_split_log2n(20) == 31
+    try:
+        h = 1 << 19
+        w20 = 2 * (h * 8) + (h // 2) * 8 + lib.dsp_fft_workspace_bytes(1, 19) + 255
+        assert lib.dsp_fft_workspace_bytes(1, 20) == max(w20, (1 << 20) * 8 + (1 << 10) * 8 + 8)
+    finally:
+        assert lib.dsp_fft_split_log2n(prev) == 20
     assert lib.dsp_fft_workspace_bytes(70000, 15) == 70000 * (1 << 15) * 8 + 65535 * 8
     rc = lib.dsp_fft_c2c_f32(1024, 1024, 1, 15, 1, 1 << 15, 1 << 15, 1024, None, 0, None)
     assert rc == _lib.DSP_EINVAL and "workspace" in _lib.last_error()

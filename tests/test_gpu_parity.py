@@ -930,7 +930,7 @@ def test_fft_nested_four_step(gpu):
     DFT of the rest) and in the spectrum's segment (every bin non-finite);
     the three-pass spectrum at 2^25 over three rows against numpy; Parseval
     and linearity on dense random 2^27 input; per-row non-finite flags at
-    2^25; 2^31 raises RuntimeError."""
+    2^25; 2^33 raises RuntimeError (2^31, 2^32: tests/test_gpu_fft_split.py)."""
     ops = _ops()
     n = 1 << 29
     f = [[3, 777777, n // 3, n - 5], [1, 2, n // 2, n - 1]]
@@ -1018,8 +1018,11 @@ def test_fft_nested_four_step(gpu):
     assert err <= FFT_RTOL * n / 2 * 0.75, err
     del X, want
     torch.cuda.empty_cache()
+    from dspcore import _lib
     with pytest.raises(RuntimeError):
-        ops._log2(1 << 31)
+        ops._log2(1 << 33)          # (2^31 and 2^32: the radix-2 split, test_gpu_fft_split.py)
+    with pytest.raises(RuntimeError):
+        ops._log2(1 << 31, _lib.DSP_MAX_LOG2N_FOURSTEP)   # the spectrum's limit
 
 
 def test_spectrum_four_step_matches_reference(gpu):
