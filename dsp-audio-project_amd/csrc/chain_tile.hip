@@ -823,7 +823,13 @@ bool tile_geometry_any(int64_t n_in, int64_t n_out, int K, int L, int M, int64_t
   // the kernel's identity cascade; it also keeps the bypass's non-finite
   // semantics (an inf or NaN stays within the SRC's window; the single-pass
   // repair would carry it into every later state of the padding stages).
-  if (S < 1 || S > kS || n_in < 1 || n_out < 1 || n_in % 4 || L < 1 || M < 1 || K < 1) return false;
+  if (S < 1 || S > kS || n_in < 1 || n_out < 1 || L < 1 || M < 1 || K < 1) return false;
+  // n_in a multiple of 4 (the rows' float4 windows), but for the one-tap SRC
+  // bypass: its x loads stop at the row's end by the buffer range check, per
+  // dword (tools/probe_buffer_oob.hip), so any length runs -- one row, or
+  // rows whose pitch is a multiple of 4 (launch_chain_tile checks)
+  const bool one_tap = L == 1 && M == 1 && K == 1 && c == 0;
+  if (n_in % 4 && !one_tap) return false;
   // SRC bypass (L = M = 1): only as the one-tap SRC (K = 1, c = 0; the
   // caller passes the tap 1.0), which the per-phase entry of the cascade alone
   // serves (chain_pp.h); any other L = M = 1 call takes the two-launch chain.
@@ -1452,8 +1458,9 @@ int launch_chain_tile(const float* x, float* y, float* z, int64_t B, int64_t n_i
   const uint64_t key0 = tables_key(tp, n_in, n_out, K, L, M, c, sos, S);
   const bool dly = key == dly_key(key0);
   if (key != key0 && !dly) return kNotFused;
-  auto aligned = [](const void* p, int64_t ld) {
-    return (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  // (one row: its pitch addresses nothing)
+  auto aligned = [B](const void* p, int64_t ld) {
+    return (B == 1 || (ld & 3) == 0) && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   };
   if (!aligned(x, ld_x) || (y && !aligned(y, ld_y)) || !aligned(z, ld_y)) return kNotFused;
   SosParams p;

@@ -244,8 +244,8 @@ class Chain:
         callers that replay graphs or pipeline many calls pass False and call
         check() themselves."""
         x = self.check_input(x)
-        if self.identity_src and (self.tile_len == 0 or ops.ld(x) % 4 or x.data_ptr() % 16
-                                  or _lib.chain_path() == 1):
+        if self.identity_src and (self.tile_len == 0 or (self.B > 1 and ops.ld(x) % 4)
+                                  or x.data_ptr() % 16 or _lib.chain_path() == 1):
             # SRC bypass (dsp_core.py:144-145) without the single-pass kernel
             # (the EQ bypassed too, dsp_chain_tile_len 0, rows of x not
             # 16-byte aligned, or dsp_chain_path(1)): y is x itself, the

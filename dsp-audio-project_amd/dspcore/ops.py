@@ -222,7 +222,7 @@ def _eq_tile_plan(n: int, sos: np.ndarray, device: torch.device):
     """(device tables, key, one-tap taps) of the single-pass cascade alone for
     rows of n samples (dsp_chain_tile_tables for the SRC bypass as the one-tap
     SRC, include/dspcore.h), cached; None where no single-pass kernel serves
-    it (n % 4, S outside 1..6, a b0 == 0 band, shared poles)."""
+    it (S outside 1..6, a b0 == 0 band, shared poles)."""
     import ctypes
     S = sos.shape[0]
     lib = _lib.load()
@@ -318,7 +318,7 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
         x = x.float()
     sos = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 5)
     B, n = x.shape
-    if B == 0 or ld(x) % 4 or x.data_ptr() % 16:
+    if B == 0 or (B > 1 and ld(x) % 4) or x.data_ptr() % 16:
         return None
     plan = _eq_tile_plan(n, sos, x.device)
     if plan is None:
@@ -326,7 +326,7 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     tables, key, taps = plan
     if out is None:
         out = torch.empty((B, n), dtype=torch.float32, device=x.device)
-    if ld(out) % 4 or out.data_ptr() % 16 or out.stride(1) != 1:
+    if (B > 1 and ld(out) % 4) or out.data_ptr() % 16 or out.stride(1) != 1:
         return None
     lib = _lib.load()
     S = sos.shape[0]

@@ -343,10 +343,11 @@ def aplicar_ecuacion_diferencias(x_n, b, a):
 def sistema_ecualizador(x_n, fs, ganancias_bandas):
     """6-band peaking-EQ cascade + clip to [-1, 1] (dsp_core.py:216-254).
 
-    Rows of a multiple of 4 samples run the single-pass kernel of the cascade
-    alone (ops.eq_single_pass: x read once, z written once; a single long
-    channel, as app.py:167 passes, takes its three-launch mode instead of
-    chained tiles); other rows the two-pass cascade (ops.biquad_cascade)."""
+    One channel of any length, or rows of a multiple of 4 samples, run the
+    single-pass kernel of the cascade alone (ops.eq_single_pass: x read once,
+    z written once; a single long channel, as app.py:167 passes, takes its
+    three-launch mode instead of chained tiles); other batches the two-pass
+    cascade (ops.biquad_cascade)."""
     plan = _design.eq_plan(fs, ganancias_bandas)
     if plan.bypass:
         return x_n

@@ -238,7 +238,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  *
  * Single-pass path (default).  When dsp_chain_tile_len() is nonzero, i.e.
  * 1 <= S <= 6 with every b0 != 0 (ABI 2.6: S = 0, the EQ bypassed, takes the
- * two-launch chain's copy pass), n_in a multiple of 4, and
+ * two-launch chain's copy pass), n_in a multiple of 4 (any n_in for the
+ * one-tap SRC bypass below), and
  *   48: (L, M, ceil(K/L)) = (3, 2, 41), c_offset mod 3 == 0,
  *       (c_offset/3 - 40) mod 4 == 0 and n_out a multiple of 4 (the kernel
  *       with wave-uniform taps: configs 3 and 4), or
@@ -260,7 +261,8 @@ int dsp_stft_mag_f32(const float* x, float* mag, int64_t B, int64_t ld_x,
  * L, M, c_offset, S or sos differ from the tables' has another key and takes
  * the two-launch path; the taps must be the ones the tables were built from),
  * and the rows of x, y and z are 16-byte aligned with pitches that are
- * multiples of 4 (n_out itself need not be), ONE kernel computes y and z from
+ * multiples of 4 (n_out itself need not be; with B == 1 the pitch is not
+ * used), ONE kernel computes y and z from
  * x: x is read once, y and z are written once, y is never read back.  Its y
  * is bitwise that of dsp_src_polyphase_f32; z agrees with the two-launch
  * chain's within 2e-6 (its carry sums run in float32 in input-normal

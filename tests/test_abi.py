@@ -197,6 +197,8 @@ def test_chain_path_tile_len_and_workspace_query():
     assert lib.dsp_chain_tile_len(48000, 48000, 1, 1, 1, 0, 6) == 48
     assert lib.dsp_chain_tile_len(48000, 48000, 41, 1, 1, 20, 6) == 0
     assert lib.dsp_chain_tile_len(48000, 48000, 1, 1, 1, 0, 0) == 0
+    assert lib.dsp_chain_tile_len(454231, 454231, 1, 1, 1, 0, 6) == 48   # any length (one tap)
+    assert lib.dsp_chain_tile_len(47999, 71998, 121, 3, 2, 60, 6) == 0   # n_in % 4 with an SRC
     B, n_in, n_out = 4096, 48000, 72000
     tiles = -(-n_out // 3072)
     ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)

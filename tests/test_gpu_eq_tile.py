@@ -459,3 +459,44 @@ def test_library_dtype_conversions(gpu):
     assert tc.shape == (50, 100)
     np.testing.assert_array_equal(tc.cpu().numpy().view(np.uint32),
                                   c.astype(np.complex64).view(np.uint32))
+
+
+@pytest.mark.parametrize("B,n_in", [(1, 441001), (1, 3073), (1, 97), (1, 48002), (3, 48001)])
+def test_cascade_alone_any_length(gpu, B, n_in):
+    """The one-tap single-pass cascade for rows whose length is not a multiple
+    of 4 (an arbitrary clip): one row runs it (its x loads stop at the row's
+    end by the buffer range check), a batch of such rows (pitch not a
+    multiple of 4) the two-pass cascade; both within 1e-5 of the oracle, a
+    NaN at the last sample relabelled as the two-pass cascade does."""
+    from dspcore.chain import Chain, ChainConfig
+    from oracle import dsp_ref_cpu as orc
+    import modules.dsp_core as dc
+    n_fft = 4096 if n_in >= 3000 else 128
+    cfg = ChainConfig(n_in, 48000, 1, 1, None, orc.CONFIG3_GAINS, n_fft=n_fft)
+    ch = Chain(cfg, B, gpu)
+    assert ch.tile_len == 48
+    gen = torch.Generator(device=gpu).manual_seed(n_in)
+    x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
+    x[0, -1] = float("nan")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        (_, z1, _), names = _traced(lambda: ch.run(x))
+        (_, z0, _), _ = _traced(lambda: ch.run_stages(x))
+    assert ("chain_tile" in names) == (B == 1), names
+    a, b = z1.cpu().numpy(), z0.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    fin = np.isfinite(b)
+    assert np.max(np.abs(a[fin] - b[fin])) <= 2e-6
+    xh = x.cpu().numpy()
+    for r in range(B):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            rz = orc.equaliser(xh[r].astype(np.float64), 48000, orc.CONFIG3_GAINS)
+        np.testing.assert_array_equal(np.isnan(a[r]), np.isnan(rz))
+        f = np.isfinite(rz)
+        assert np.max(np.abs(a[r][f] - rz[f])) <= EQ_ATOL
+    # the drop-in on the numpy row (one channel: the single-pass kernel)
+    xs = xh[0].astype(np.float64)
+    xs[-1] = 0.25
+    z = dc.sistema_ecualizador(xs, 48000, orc.CONFIG3_GAINS)
+    assert np.max(np.abs(z - orc.equaliser(xs, 48000, orc.CONFIG3_GAINS))) <= EQ_ATOL
