@@ -332,7 +332,10 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     S = sos.shape[0]
     chunk = chunk_len_for(n, max_chunks_for(B))
     ws_bytes = int(lib.dsp_chain_workspace_bytes(B, n, n, 1, 1, 1, 0, S, chunk))
-    ws = _eq_workspace(x.device, ws_bytes)
+    # (reused only where a give-up is detected and the workspace reset: a flag
+    # a give-up left raised would mislead the next call's tiles)
+    ws = (_eq_workspace(x.device, ws_bytes) if check else
+          torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device))
     force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S, B)
     with torch.cuda.device(x.device), force:
         rc = lib.dsp_chain_f32(
