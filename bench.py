@@ -43,7 +43,9 @@ chain kernel's 1 read : 2 writes mix, tools/ubench_rw_mix in a child
 process; roofline.frac_vs_mix_ceiling), `fft_2_28` (the three-pass FFT of
 one 2^28-point row: ms and its algorithmic rate; not part of the metric),
 `app_rerun` (one channel through the drop-in as app.py calls it, next to the
-oracle) and `ratio_sweep` (every L/M in 1..8 at 4096 channels: path taken
+oracle), `eq_alone` (the sliders' default L = M = 1: the single-pass cascade
+alone at 32768 x 48000 and on one 441000-sample channel, against the two-pass
+cascade) and `ratio_sweep` (every L/M in 1..8 at 4096 channels: path taken
 and Msamples/s against the two-launch chain).  DSP_BENCH_DRYRUN=1 replaces the GPU measurement by a stub
 (tests of the rank launcher and sharding on CPU).
 """
@@ -475,6 +477,70 @@ def copy_ceiling(device, nbytes=1 << 30, reps=20):
                    f"mean of {reps} after 3 warm, CUDA events"}
 
 
+def eq_alone(device, reps=10):
+    """The app's default ratio L = M = 1 (app.py:149-150): the SRC returns x
+    and sistema_ecualizador (dsp_core.py:216-254) is the whole path, here the
+    single-pass one-tap cascade with the config-3 gains and
+    no spectrum, graph-replayed: 32768 x 48000 (chained tiles; algorithmic
+    bytes 8 per sample, x read and z written, against 8 TB/s) and one
+    441000-sample channel (the three-launch mode), each beside the two-pass
+    cascade (k_iir_wave) on the same input.  Not the metric."""
+    import torch
+
+    from dspcore import ops
+    from dspcore.design import eq_plan
+
+    sos = eq_plan(48000, CONFIG3_GAINS).sos
+
+    def graph_ms(fn):
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            fn()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                fn()
+        torch.cuda.current_stream(device).wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize(device)
+        return e0.elapsed_time(e1) / reps
+
+    out = {}
+    with torch.cuda.device(device):
+        for tag, B, n in (("32768x48000", 32768, 48000), ("1x441000", 1, 441000)):
+            x = torch.rand((B, n), device=device) * 2 - 1
+            z = torch.empty_like(x)
+            ws = ops.biquad_workspace(B, n, sos.shape[0], device)
+            if ops.eq_single_pass(x, sos, out=z) is None:
+                return None
+            t1 = graph_ms(lambda: ops.eq_single_pass(x, sos, out=z))
+            t0 = graph_ms(lambda: ops.biquad_cascade(x, sos, True, out=z, workspace=ws))
+            gbs = B * n * 8 / (t1 * 1e-3) / 1e9
+            out[tag] = {"single_pass_ms": round(t1, 4), "two_pass_ms": round(t0, 4),
+                        "speedup": round(t0 / t1, 2),
+                        "msamples_s": round(B * n / (t1 * 1e-3) / 1e6, 1),
+                        "algorithmic_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "mode": "three-launch" if _lib_mode(B, n, sos.shape[0]) == 3 else
+                                "chained tiles"}
+            del x, z, ws
+            torch.cuda.empty_cache()
+    out["how"] = ("ops.eq_single_pass (dsp_chain_f32 with the one-tap SRC bypass, y and mag NULL) "
+                  "vs ops.biquad_cascade, config-3 gains at 48 kHz, HIP graph replays, mean of "
+                  f"{reps}; algorithmic bytes 8 per sample")
+    return out
+
+
+def _lib_mode(B, n, S):
+    from dspcore import _lib
+    return _lib.load().dsp_chain_mode(B, n, n, 1, 1, 1, 0, S)
+
+
 def fft_large(device, log2n=28, reps=3):
     """The three-pass four-step FFT of one complex row of 2^log2n points
     (fft_diezmado_en_tiempo's size range above one workgroup's LDS): ms per
@@ -790,6 +856,7 @@ def main(argv=None):
             torch.cuda.empty_cache()
         extras["host_inclusive"] = host_inclusive(device)
         extras["app_rerun"] = app_rerun(device)
+        extras["eq_alone"] = eq_alone(device)
         if not args.no_sweep:
             extras["ratio_sweep"] = ratio_sweep(device)
         extras["copy_ceiling"] = copy_ceiling(device)
@@ -856,6 +923,7 @@ def main(argv=None):
             **{k: extras.get(k) for k in ("config3", "config4", "config5") if k in extras},
             "host_inclusive": extras.get("host_inclusive"),
             "app_rerun": extras.get("app_rerun"),
+            "eq_alone": extras.get("eq_alone"),
             **({"ratio_sweep": extras["ratio_sweep"]} if extras.get("ratio_sweep") else {}),
             "copy_ceiling": extras.get("copy_ceiling"),
             "mix_ceiling": extras.get("mix_ceiling"),
