@@ -199,6 +199,18 @@ def test_chain_path_tile_len_and_workspace_query():
     assert lib.dsp_chain_tile_len(48000, 48000, 1, 1, 1, 0, 0) == 0
     assert lib.dsp_chain_tile_len(454231, 454231, 1, 1, 1, 0, 6) == 48   # any length (one tap)
     assert lib.dsp_chain_tile_len(47999, 71998, 121, 3, 2, 60, 6) == 0   # n_in % 4 with an SRC
+    # dsp_chain_mode (host): the default's single-pass mode for a batch -- the
+    # three-launch mode for a few long rows, chained tiles for full batches
+    # (DESIGN.md §3.0.9), 0 where the two-launch chain serves the geometry
+    assert lib.dsp_chain_mode(1, 441000, 441000, 1, 1, 1, 0, 6) == 3          # the EQ alone
+    assert lib.dsp_chain_mode(32768, 48000, 48000, 1, 1, 1, 0, 6) == 1
+    assert lib.dsp_chain_mode(16, 441000, 661500, 121, 3, 2, 60, 6) == 3      # L3/M2 kernel
+    assert lib.dsp_chain_mode(32768, 48000, 72000, 121, 3, 2, 60, 6) == 1     # config 4
+    assert lib.dsp_chain_mode(2, 441000, 882000, 81, 2, 1, 40, 6) == 3        # per-phase 2/1
+    assert lib.dsp_chain_mode(1, 441000, 480000, 1023, 160, 147, 511, 6) == 3  # generic
+    assert lib.dsp_chain_mode(8192, 48000, 52245, 1023, 160, 147, 511, 6) == 1  # config 5
+    assert lib.dsp_chain_mode(1, 48000, 44100, 1023, 147, 160, 511, 6) == 0   # two-launch
+    assert lib.dsp_chain_mode(0, 48000, 72000, 121, 3, 2, 60, 6) == 0
     B, n_in, n_out = 4096, 48000, 72000
     tiles = -(-n_out // 3072)
     ws = lib.dsp_chain_workspace_bytes(B, n_in, n_out, 121, 3, 2, 60, 6, 1152)
