@@ -25,7 +25,13 @@ def short(name):
         return "lfilter_nf"
     if "k_pcm_batch" in name or "k_scale_batch" in name:
         return "pcm_batch"
-    if "k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gc" in name:
+    if "k_chain_tile_carry" in name or "k_tile_carry" in name:
+        return "chain_tile_carry"
+    if ("k_chain_pp3" in name or "k_chain_tile3" in name or "k_chain_gen3" in name or
+            "k_chain_gct3" in name):
+        return "chain_tile3"
+    if ("k_chain_tile" in name or "k_chain_gen" in name or "k_chain_gc" in name or
+            "k_chain_pp" in name):
         return "chain_tile"
     if "k_tile_prep" in name:
         return "chain_prep"
