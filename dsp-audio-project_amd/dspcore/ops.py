@@ -96,7 +96,10 @@ def taps_tensor(plan: SrcPlan, device: torch.device) -> torch.Tensor:
     """The library's float32 taps (design.caller_taps; it flushes the sinc-zero
     noise itself, design.kernel_taps)."""
     from .design import caller_taps
-    return torch.from_numpy(caller_taps(plan)).to(device)
+    host = caller_taps(plan)
+    # cached: the app's reruns take the same few designs (one fewer copy a call)
+    return _cached(("taps", host.tobytes(), device.index),
+                   lambda: torch.from_numpy(host).to(device))
 
 
 def src_polyphase(x: torch.Tensor, plan: SrcPlan, taps: torch.Tensor | None = None,
@@ -343,7 +346,11 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
             _lib.sos_pointer(sos), S, 1, chunk, None, None, 0, _ptr(tables), key, 0, 0, 0, 0,
             None, None, _ptr(ws), ws.numel(), _stream(x.device))
         _lib.check(rc, "dsp_chain_f32")
-        if check:
+        # the three-launch mode has no hand-off wait that could give up: no
+        # status read (and no stream synchronisation) for it
+        path = _lib.chain_path()
+        if check and not (path == 4 or (path == 0 and lib.dsp_chain_mode(
+                B, n, n, 1, 1, 1, 0, S) == 3)):
             st = lib.dsp_chain_status(_ptr(ws), ws.numel(), 0, _stream(x.device))
             if st < 0:
                 _lib.check(st, "dsp_chain_status")
@@ -469,6 +476,53 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
                                   0 if ws is None else ws.numel(), _stream(x.device))
     _lib.check(rc, "dsp_spectrum_f32")
     return out
+
+
+# Page-locked staging buffers of spectrum_host, per thread and device (grown,
+# never shrunk; calls are synchronous, so a thread's next call may reuse them).
+_host_stage = threading.local()
+# spectrum_host takes segments up to this many bytes (float32) per call.
+SPECTRUM_HOST_MAX_BYTES = 4 << 20
+
+
+def _pinned(slot: str, device: torch.device, nbytes: int) -> torch.Tensor:
+    bufs = getattr(_host_stage, "bufs", None)
+    if bufs is None:
+        bufs = _host_stage.bufs = {}
+    key = (slot, device.index)
+    t = bufs.get(key)
+    if t is None or t.numel() < nbytes:
+        t = bufs[key] = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
+    return t
+
+
+def spectrum_host(seg: np.ndarray, n_fft: int, device: torch.device) -> np.ndarray | None:
+    """|FFT(hann * row)|[:n_fft/2+1] of every row of a host array [B, seg_len]
+    (the already-cut segments of dsp_core.py:76-82), float32, for a few small
+    segments: the rows go, cast to float32 by numpy (astype's rounding, as
+    `convert`), into page-locked host memory that the spectrum kernel reads
+    directly over the bus, and the kernel writes |X| into page-locked memory
+    too -- no copy launches, one stream synchronisation.  None when the call
+    is not of that kind (the caller takes the device path)."""
+    B, seg_len = seg.shape
+    half = n_fft // 2 + 1
+    lg = _log2(n_fft, _lib.DSP_MAX_LOG2N_FOURSTEP)
+    if B < 1 or lg > _lib.DSP_MAX_LOG2N or B * max(seg_len, half) * 4 > SPECTRUM_HOST_MAX_BYTES:
+        return None
+    xin = _pinned("spec_in", device, max(B * seg_len * 4, 16))
+    xout = _pinned("spec_out", device, B * half * 4)
+    xv = xin.numpy()[:B * seg_len * 4].view(np.float32).reshape(B, seg_len)
+    np.copyto(xv, seg, casting="unsafe")
+    win = _table("hann", n_fft, device)
+    tw = _table("tw", n_fft, device)
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        stream = torch.cuda.current_stream(device)
+        rc = lib.dsp_spectrum_f32(xin.data_ptr(), xout.data_ptr(), B, seg_len, 0, seg_len, lg,
+                                  half, _ptr(win), _ptr(tw), None, 0, stream.cuda_stream)
+        _lib.check(rc, "dsp_spectrum_f32")
+        stream.synchronize()
+    return xout.numpy()[:B * half * 4].view(np.float32).reshape(B, half).copy()
 
 
 def stft_magnitude(x: torch.Tensor, n_fft: int, hop: int, frames: int,

@@ -4,8 +4,14 @@ route (host dtype conversion + pageable copies) against device-side casts and
 pinned (page-locked) host buffers.  ms per variant, median of 20."""
 import time
 
+import os
+import sys
+
 import numpy as np
 import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "dsp-audio-project_amd"))
 
 
 def med(fn, k=20):
@@ -21,6 +27,7 @@ def med(fn, k=20):
 
 
 def main():
+    from dspcore import ops
     dev = torch.device("cuda", 0)
     for n in (441000, 882000):
         t = torch.rand(n, device=dev)
@@ -38,6 +45,11 @@ def main():
                     t.to(torch.float64)).numpy(),
             "device cast f64 + D2H into held pinned":
                 lambda: pin64.copy_(t.to(torch.float64)).numpy(),
+            "library cast kernel writing f64 into held pinned (zero-copy)":
+                lambda: ops.convert(t, torch.float64, out=pin64).numpy(),
+            "library cast kernel writing f64 into fresh pinned (zero-copy)":
+                lambda: ops.convert(t, torch.float64, out=torch.empty(
+                    n, dtype=torch.float64, pin_memory=True)).numpy(),
             "D2H f32 into held pinned + host astype":
                 lambda: pin32.copy_(t).numpy().astype(np.float64),
             "H2D: host astype f32 + pageable (current, f64 in)":
