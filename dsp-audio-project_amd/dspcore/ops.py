@@ -478,10 +478,11 @@ def spectrum(x: torch.Tensor, seg_start: int, seg_len: int, n_fft: int,
     return out
 
 
-# Page-locked staging buffers of spectrum_host, per thread and device (grown,
-# never shrunk; calls are synchronous, so a thread's next call may reuse them).
+# Page-locked staging buffers of spectrum_host / fft_host, per thread and
+# device (grown, never shrunk; calls are synchronous, so a thread's next call
+# may reuse them).
 _host_stage = threading.local()
-# spectrum_host takes segments up to this many bytes (float32) per call.
+# spectrum_host / fft_host take up to this many bytes (float32 / complex64) per call.
 SPECTRUM_HOST_MAX_BYTES = 4 << 20
 
 
@@ -496,14 +497,16 @@ def _pinned(slot: str, device: torch.device, nbytes: int) -> torch.Tensor:
     return t
 
 
-def spectrum_host(seg: np.ndarray, n_fft: int, device: torch.device) -> np.ndarray | None:
+def spectrum_host(seg: np.ndarray, n_fft: int, device: torch.device,
+                  out_dtype=np.float32) -> np.ndarray | None:
     """|FFT(hann * row)|[:n_fft/2+1] of every row of a host array [B, seg_len]
     (the already-cut segments of dsp_core.py:76-82), float32, for a few small
     segments: the rows go, cast to float32 by numpy (astype's rounding, as
     `convert`), into page-locked host memory that the spectrum kernel reads
     directly over the bus, and the kernel writes |X| into page-locked memory
-    too -- no copy launches, one stream synchronisation.  None when the call
-    is not of that kind (the caller takes the device path)."""
+    too -- no copy launches, one stream synchronisation; returned as a fresh
+    array of out_dtype.  None when the call is not of that kind (the caller
+    takes the device path)."""
     B, seg_len = seg.shape
     half = n_fft // 2 + 1
     lg = _log2(n_fft, _lib.DSP_MAX_LOG2N_FOURSTEP)
@@ -522,7 +525,35 @@ def spectrum_host(seg: np.ndarray, n_fft: int, device: torch.device) -> np.ndarr
                                   half, _ptr(win), _ptr(tw), None, 0, stream.cuda_stream)
         _lib.check(rc, "dsp_spectrum_f32")
         stream.synchronize()
-    return xout.numpy()[:B * half * 4].view(np.float32).reshape(B, half).copy()
+    return xout.numpy()[:B * half * 4].view(np.float32).reshape(B, half).astype(out_dtype)
+
+
+def fft_host(x: np.ndarray, device: torch.device, out_dtype=np.complex64) -> np.ndarray | None:
+    """The DFT of every row of a host array [B, n] (real or complex, n a power
+    of two up to one LDS-resident launch), as spectrum_host does it: numpy
+    casts the rows (float32 / complex64, astype's rounding) into page-locked
+    memory, dsp_fft_c2c_f32 reads them and writes X there, no copy launches;
+    returned as a fresh array of out_dtype.  None when the call is not of that
+    kind (the caller takes the device path)."""
+    B, n = x.shape
+    lg = _log2(n)
+    if B < 1 or lg > _lib.DSP_MAX_LOG2N or B * n * 8 > SPECTRUM_HOST_MAX_BYTES:
+        return None
+    real = not np.iscomplexobj(x)
+    ft = np.float32 if real else np.complex64
+    nin = B * n * np.dtype(ft).itemsize
+    xin = _pinned("fft_in", device, nin)
+    xout = _pinned("fft_out", device, B * n * 8)
+    np.copyto(xin.numpy()[:nin].view(ft).reshape(B, n), x, casting="unsafe")
+    tw = _table("tw", n, device)
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        stream = torch.cuda.current_stream(device)
+        rc = lib.dsp_fft_c2c_f32(xin.data_ptr(), xout.data_ptr(), B, lg, int(real), n, n,
+                                 _ptr(tw), None, 0, stream.cuda_stream)
+        _lib.check(rc, "dsp_fft_c2c_f32")
+        stream.synchronize()
+    return xout.numpy()[:B * n * 8].view(np.complex64).reshape(B, n).astype(out_dtype)
 
 
 def stft_magnitude(x: torch.Tensor, n_fft: int, hop: int, frames: int,

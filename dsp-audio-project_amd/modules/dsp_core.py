@@ -240,6 +240,17 @@ def fft_diezmado_en_tiempo(x):
     if n & (n - 1):
         raise ValueError(f"fft_diezmado_en_tiempo: length {n} is not a power of two")
     ops = _ops()
+    if not _is_tensor(x):
+        # a few short rows: read and answered in page-locked host memory
+        # (ops.fft_host, as the spectrum's segments), no copy launches
+        a = np.asarray(x)
+        if a.ndim in (1, 2) and (a.ndim == 1 or a.shape[0] < SHARD_MIN_ROWS
+                                 or len(_shard_devices()) <= 1):
+            import torch
+            X = ops.fft_host(a[None, :] if a.ndim == 1 else a,
+                             torch.device("cuda", torch.cuda.current_device()), np.complex128)
+            if X is not None:
+                return X[0] if a.ndim == 1 else X
     return _run(x, lambda t, B: ops.fft(t), np.complex128, complex_ok=True)
 
 
@@ -266,9 +277,9 @@ def calcular_espectro_magnitud(x_n, fs, *, n_fft: int = _design.SPECTRUM_WINDOW)
                                  or len(_shard_devices()) <= 1):
                 import torch
                 mag = ops.spectrum_host(seg[None, :] if a.ndim == 1 else seg, plan.n_fft,
-                                        torch.device("cuda", torch.cuda.current_device()))
+                                        torch.device("cuda", torch.cuda.current_device()),
+                                        np.float64)
                 if mag is not None:
-                    mag = mag.astype(np.float64)
                     return freqs, (mag[0] if a.ndim == 1 else mag)
             x_n = np.ascontiguousarray(seg)
     mag = _run(x_n, lambda t, B: ops.spectrum(t, seg_start, plan.seg_len, plan.n_fft),
