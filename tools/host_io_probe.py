@@ -59,6 +59,10 @@ def main():
             "H2D: f64 via held pinned + device cast":
                 lambda: (pin64.numpy().__setitem__(slice(None), a64),
                          pin64.to(dev, non_blocking=True).float())[1],
+            "H2D: f64 from a numpy view of pinned memory + device cast":
+                lambda: torch.from_numpy(pin64.numpy()).to(dev).float(),
+            "H2D: f64 pinned tensor non_blocking + device cast":
+                lambda: pin64.to(dev, non_blocking=True).float(),
             "H2D: f32 pageable (f32 in)":
                 lambda: torch.from_numpy(a32).to(dev),
             "H2D: f32 via held pinned":
