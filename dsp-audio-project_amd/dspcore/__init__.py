@@ -13,7 +13,7 @@ The reference-compatible drop-in is dsp-audio-project_amd/modules/dsp_core.py.
 from . import design  # noqa: F401
 
 __all__ = ["design", "ops", "chain", "shard", "host"]
-__version__ = "1.5.0"
+__version__ = "1.6.0"
 
 
 def __getattr__(name):  # lazy: importing design must not require the GPU library
