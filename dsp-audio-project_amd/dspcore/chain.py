@@ -155,6 +155,20 @@ class Chain:
                 self.tile_key = int(key.value)
             else:
                 self.tile_len = 0
+        # Geometries without a single-pass SRC kernel (e.g. 48 -> 44.1 kHz,
+        # L/M = 147/160 at K = 1023): the SRC kernel writes y and the
+        # single-pass cascade alone (the one-tap kernel, ops.eq_single_pass)
+        # reads it once, instead of the library's two-launch chain (x-domain
+        # chunk states, then the cascade's pass 2 over y): 147/160 at 8192
+        # channels 1.949 -> 1.659 ms (tools/two_launch_ident.py).
+        # dsp_chain_path(1) still selects the library's two-launch chain.
+        self._plan_batch = None if plan_batch is None else int(plan_batch)
+        self._split_ws = None
+        if (self.tile_len == 0 and not self.identity_src and not self.eq.bypass
+                and ops._eq_tile_plan(n_out, self.sos, dev) is not None):
+            nb = lib.dsp_chain_workspace_bytes(self.B, n_out, n_out, 1, 1, 1, 0, S,
+                                               chunk_len_for(n_out, max_chunks_for(self.B)))
+            self._split_ws = torch.zeros(max(int(nb), 256), dtype=torch.uint8, device=dev)
         # y: the caller's output, or the two-launch chain's intermediate; with
         # keep_y=False on the single-pass path it is never allocated, and with
         # the SRC bypass it is x.
@@ -205,13 +219,17 @@ class Chain:
 
     def _status(self, reset: bool) -> int:
         lib = _lib.load()
-        with torch.cuda.device(self.device):
-            rc = lib.dsp_chain_status(self.workspace.data_ptr(), self.workspace.numel(),
-                                      int(bool(reset)),
-                                      torch.cuda.current_stream(self.device).cuda_stream)
-        if rc < 0:
-            _lib.check(rc, "dsp_chain_status")
-        return rc
+        total = 0
+        for ws in (self.workspace, self._split_ws):
+            if ws is None:
+                continue
+            with torch.cuda.device(self.device):
+                rc = lib.dsp_chain_status(ws.data_ptr(), ws.numel(), int(bool(reset)),
+                                          torch.cuda.current_stream(self.device).cuda_stream)
+            if rc < 0:
+                _lib.check(rc, "dsp_chain_status")
+            total += rc
+        return total
 
     def handoff_ok(self) -> bool:
         """False if a single-pass call's tile hand-off wait gave up since the
@@ -254,6 +272,21 @@ class Chain:
             if z is not self.z:
                 self.z.copy_(z)         # the EQ bypassed too: z is x (run_stages)
             return (x if self.keep_y else None), self.z, self.mag
+        if self._split_ws is not None and _lib.chain_path() != 1:
+            # SRC kernel, then the single-pass cascade alone on y (__init__)
+            with torch.cuda.device(self.device):
+                ops.src_polyphase(x, self.src, self.taps, out=self.y)
+                if ops.eq_single_pass(self.y, self.sos, out=self.z, plan_batch=self._plan_batch,
+                                      workspace=self._split_ws) is None:
+                    raise RuntimeError("single-pass cascade declined the chain's own y / z")
+                ops.spectrum(self.z, self.spec.seg_start, self.spec.seg_len, self.spec.n_fft,
+                             out=self.mag)
+                self._extra_spectra(x, self.y)
+            if check is None:
+                check = not torch.cuda.is_current_stream_capturing()
+            if check:
+                self.check()
+            return (self.y if self.keep_y else None), self.z, self.mag
         lib = _lib.load()
         sos_ptr = _lib.sos_pointer(self.sos)
         S = self.sos.shape[0]

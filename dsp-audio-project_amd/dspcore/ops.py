@@ -306,7 +306,8 @@ def _eq_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = None,
-                   plan_batch: int | None = None, check: bool = False) -> torch.Tensor | None:
+                   plan_batch: int | None = None, check: bool = False,
+                   workspace: torch.Tensor | None = None) -> torch.Tensor | None:
     """z = clip(cascade(x)) per row (dsp_core.py:233-254) through the
     single-pass kernel of the cascade alone: dsp_chain_f32 with the SRC bypass
     as the one-tap SRC (L = M = 1, K = 1, tap 1.0), y = NULL, mag = NULL -- x
@@ -315,7 +316,10 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     forced_chain_path).  Returns None where that kernel does not serve the
     call (biquad_cascade does) -- and, with check (it synchronises the
     stream), where a chained tile's hand-off wait gave up (dsp_chain_status;
-    the workspace is reset): the caller reruns the rows on biquad_cascade."""
+    the workspace is reset): the caller reruns the rows on biquad_cascade.
+    workspace: the caller's zero-filled chain workspace of at least
+    dsp_chain_workspace_bytes for this call, used on one stream (every call
+    that completes leaves it clear); by default one is made or reused here."""
     x = _rows(x, "x")
     if x.dtype != torch.float32:
         x = x.float()
@@ -337,8 +341,13 @@ def eq_single_pass(x: torch.Tensor, sos: np.ndarray, out: torch.Tensor | None = 
     ws_bytes = int(lib.dsp_chain_workspace_bytes(B, n, n, 1, 1, 1, 0, S, chunk))
     # (reused only where a give-up is detected and the workspace reset: a flag
     # a give-up left raised would mislead the next call's tiles)
-    ws = (_eq_workspace(x.device, ws_bytes) if check else
-          torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device))
+    if workspace is not None:
+        if workspace.numel() < ws_bytes or not workspace.is_cuda:
+            raise ValueError(f"workspace of {workspace.numel()} bytes < {ws_bytes}")
+        ws = workspace
+    else:
+        ws = (_eq_workspace(x.device, ws_bytes) if check else
+              torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=x.device))
     force = forced_chain_path(plan_batch if plan_batch != B else None, n, n, 1, 1, 1, 0, S, B)
     with torch.cuda.device(x.device), force:
         rc = lib.dsp_chain_f32(

@@ -563,9 +563,10 @@ def test_chain_generic_single_pass(gpu, n_in, fs, L, M, K, B):
 def test_chain_two_launch_48k_to_44k1(gpu):
     """48 kHz -> 44.1 kHz (L/M = 147/160, K = 1023): 147 phase classes of the
     32-output sub-chunks are more than the single-pass kernels' LDS tables
-    hold, so the chain plans the two-launch path (SRC kernel, then the
-    cascade); its rows against the reference recipe (dsp_core.py:133-173,
-    216-254, 68-98), clip driven."""
+    hold, so no single-pass SRC kernel serves it: Chain runs the SRC kernel,
+    then the single-pass cascade alone on y; its rows against the library's
+    two-launch chain and the reference recipe (dsp_core.py:133-173, 216-254,
+    68-98), clip driven."""
     from dspcore.chain import Chain, ChainConfig
     from oracle import dsp_ref_cpu as orc
     B, n_in = 3, 9600
@@ -575,7 +576,17 @@ def test_chain_two_launch_48k_to_44k1(gpu):
     gen = torch.Generator(device=gpu).manual_seed(147)
     x = torch.rand((B, n_in), generator=gen, device=gpu) * 2 - 1
     x[1] *= 40.0
-    y, z, mag = (t.cpu().numpy() for t in ch.run(x))
+    # the SRC kernel, then the single-pass cascade alone on y (Chain's route
+    # for geometries without a single-pass SRC kernel), against the library's
+    # two-launch chain: y bitwise, z within 2e-6
+    (y, z, mag), names = _traced(lambda: ch.run(x))
+    assert "src_poly" in names and "chain_tile" in names, names
+    with _chain_path(1):
+        (y1, z1, m1), names1 = _traced(lambda: ch.run(x))
+    assert "chain_tile" not in names1, names1
+    assert torch.equal(y, y1) and (z - z1).abs().max().item() <= 2e-6
+    assert (mag - m1).abs().max().item() <= 1e-5 * m1.abs().max().item()
+    y, z, mag = (t.cpu().numpy() for t in (y, z, mag))
     for b in range(B):
         ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 147, 160, orc.CONFIG3_GAINS,
                                        1023, 2048)
@@ -646,9 +657,12 @@ def test_chain_single_pass_fewer_bands_and_bypass(gpu, gains):
 
 def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
     """x rows that are not 16-byte aligned (n_in % 4 != 0) cannot feed the
-    x-domain chunk states; the chain then uses the y-domain table (the
+    x-domain chunk states nor the single-pass SRC kernels.  The library's
+    two-launch chain (dsp_chain_path(1)) then uses the y-domain table (the
     contract in include/dspcore.h) instead of failing, bitwise equal to the
-    staged path, and still matches the reference recipe."""
+    staged path; the default (Chain: the SRC kernel, then the single-pass
+    cascade alone on y) has the same y and z within 2e-6 of it; both match
+    the reference recipe."""
     from dspcore.chain import Chain, ChainConfig
     from oracle import dsp_ref_cpu as orc
     n_in = 47999
@@ -656,10 +670,16 @@ def test_chain_unaligned_input_rows_fall_back_to_y_states(gpu):
     ch = Chain(cfg, 3, gpu)
     gen = torch.Generator(device=gpu).manual_seed(13)
     x = torch.rand((3, n_in), generator=gen, device=gpu) * 2 - 1
-    assert ch.tile_len == 0           # n_in % 4 != 0: the two-launch chain
-    y, z, mag = (t.clone() for t in ch.run(x))
+    assert ch.tile_len == 0           # n_in % 4 != 0: no single-pass SRC kernel
+    with _chain_path(1):
+        (y, z, mag), names1 = _traced(lambda: ch.run(x))
+    assert "src_poly" in names1 and "chain_tile" not in names1, names1
     y2, z2, m2 = ch.run_stages(x)
     assert torch.equal(y, y2) and torch.equal(z, z2) and torch.equal(mag, m2)
+    (y3, z3, m3), names = _traced(lambda: ch.run(x))
+    assert "src_poly" in names and "chain_tile" in names, names
+    assert ch.handoff_ok()
+    assert torch.equal(y3, y) and (z3 - z).abs().max().item() <= 2e-6
     for b in range(3):
         ry, rz, _, rmag, _ = orc.chain(x[b].cpu().numpy(), 48000, 3, 2, orc.CONFIG3_GAINS,
                                        None, 4096)
