@@ -54,9 +54,10 @@ def test_app_rerun_every_ratio(gpu, L, M):
         got = _spectrum_or_error(dc.calcular_espectro_magnitud, v[:lim], f)
         if seg & (seg - 1):
             # a segment that is not a power of two: the reference's recursion
-            # raises (or, for 3 * 2^k, returns a wrong-length array), the
-            # drop-in raises ValueError (deliberate differences)
+            # raises there (dsp_core.py:55-64 adds halves of unequal length),
+            # and so does the drop-in (design.spectrum_plan)
             assert got is None, (n_v, seg)
+            assert _spectrum_or_error(orc.spectrum, rv[:lim], f) is None, (n_v, seg)
             continue
         (fg, mg), (fr, mr) = got, orc.spectrum(rv[:lim], f)
         np.testing.assert_array_equal(fg, fr)
