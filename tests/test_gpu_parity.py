@@ -862,6 +862,43 @@ def test_shards_plan_with_the_job_batch(gpu):
     assert np.max(np.abs(own[0] - base[0])) <= 2e-6
 
 
+def test_shards_of_the_split_route_bitwise(gpu):
+    """48 -> 44.1 kHz (147/160, K = 1023: no single-pass SRC kernel; Chain runs
+    the SRC kernel, then the single-pass cascade alone on y), 512 rows of
+    48000: the job's batch takes the chained tiles, a shard of 128 by itself
+    the three-launch mode.  Planned with the job's batch every shard of 1, 2
+    and 4 forces the job's mode and the rows are bitwise the unsharded ones;
+    planned per shard they agree to float64 rounding."""
+    from dspcore import _lib
+    from dspcore.chain import Chain, ChainConfig
+    from dspcore.shard import run_sharded
+    from oracle import dsp_ref_cpu as orc
+    B, n_in = 512, 48000
+    cfg = ChainConfig(n_in, 48000, 147, 160, 1023, orc.CONFIG3_GAINS, n_fft=4096)
+    lib = _lib.load()
+    n_out = Chain(cfg, 1, gpu).n_out
+    assert lib.dsp_chain_mode(B, n_out, n_out, 1, 1, 1, 0, 6) == 1
+    assert lib.dsp_chain_mode(B // 4, n_out, n_out, 1, 1, 1, 0, 6) == 3
+    x = np.random.default_rng(147).uniform(-1, 1, (B, n_in)).astype(np.float32)
+
+    def fn(plan):
+        def run(xd):
+            ch = Chain(cfg, xd.shape[0], xd.device, plan_batch=plan)
+            assert ch.tile_len == 0 and ch._split_ws is not None
+            y, z, mag = ch.run(xd)
+            return y.clone(), z.clone(), mag.clone()
+        return run
+
+    base = run_sharded(fn(B), x, [gpu])
+    for parts in (2, 4):
+        got = run_sharded(fn(B), x, [gpu] * parts)
+        for a, b in zip(got, base):
+            np.testing.assert_array_equal(a, b)
+    own = run_sharded(fn(None), x, [gpu] * 4)
+    np.testing.assert_array_equal(own[0], base[0])          # y: one SRC kernel
+    assert np.max(np.abs(own[1] - base[1])) <= 2e-6
+
+
 def test_fft_four_step_matches_reference(gpu):
     """N = 2^13 .. 2^16 through the drop-in against the reference's own outputs
     (tests/golden/fft_large.npz; 2^15 and 2^16 take the four-step path), and
