@@ -161,10 +161,13 @@ class Chain:
         # reads it once, instead of the library's two-launch chain (x-domain
         # chunk states, then the cascade's pass 2 over y): 147/160 at 8192
         # channels 1.949 -> 1.659 ms (tools/two_launch_ident.py).
-        # dsp_chain_path(1) still selects the library's two-launch chain.
+        # dsp_chain_path(1), and a caller that picks a two-launch variant
+        # (chunk_len, use_table=False, use_xstate=False), still select the
+        # library's two-launch chain.
         self._plan_batch = None if plan_batch is None else int(plan_batch)
         self._split_ws = None
         if (self.tile_len == 0 and not self.identity_src and not self.eq.bypass
+                and chunk_len is None and use_table and use_xstate
                 and ops._eq_tile_plan(n_out, self.sos, dev) is not None):
             nb = lib.dsp_chain_workspace_bytes(self.B, n_out, n_out, 1, 1, 1, 0, S,
                                                chunk_len_for(n_out, max_chunks_for(self.B)))
