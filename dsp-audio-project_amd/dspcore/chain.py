@@ -6,7 +6,10 @@ A Chain owns every device buffer (taps, LUTs, y, z, mag, workspace) so that
 
 Where the library has a single-pass kernel for the geometry
 (dsp_chain_tile_len > 0, include/dspcore.h) one launch computes y and z from x
-and a second the spectrum; otherwise SRC, cascade and spectrum run as three.
+and a second the spectrum; otherwise the SRC kernel writes y, the single-pass
+cascade alone (the one-tap kernel) reads it once and writes z, and the
+spectrum follows -- or, with dsp_chain_path(1), an explicit two-launch
+variant, or more than six bands, the library's two-launch chain.
 
 The single-pass kernel hands each tile's carry to the next tile through the
 workspace; if a wait ever gives up (dsp_chain_status), run() raises
